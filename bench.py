@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark: HiFiGAN-v1 mel->waveform on MI355X (BASELINE.json metric / config 2).
+
+One "step" = ``HifiganGenerator.inference`` on a resident [32, 80, 1024] fp32 mel batch
+(replicate pad 5 -> 1034 frames -> 32 x 264,704 output samples), through the C-ABI library.
+One process per GPU; with N GPUs every rank vocodes its own 32-utterance shard (weak
+scaling, config 4's 256 utterances at N=8, no exchange step on the data path).
+
+Prints ONE JSON line (rank 0) with the driver contract fields plus:
+  roofline     : the dominant kernel family's algorithmic FLOP/s (hipEvent-timed inside one
+                 profiled forward, on the stream the kernels run on) vs the 157.3 TF fp32 peak
+  cpu_baseline : the CPU oracle (oracle/hifigan_ref.py, torch.nn.functional fp32, the same
+                 ATen kernels as the reference) on a bounded sample, rank 0 at N=1 only
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tts-3_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+SAMPLE_RATE = 22050
+METRIC = "audio samples/sec + RTF, HiFiGAN-v1 22.05kHz 80-mel, batch 32 @ 1/2/4/8 GPU"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=32, help="utterances per GPU")
+    p.add_argument("--frames", type=int, default=1024)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    p.add_argument("--comm", action="store_true",
+                   help="also time an RCCL scatter of mels / gather of wavs from rank 0 (reported separately)")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
+    return p.parse_args()
+
+
+def dominant_kernel(rows):
+    fam = {}
+    for r in rows:
+        f = fam.setdefault(r["name"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
+        f["ms"] += r["ms"]
+        f["flops"] += r["flops"]
+        f["bytes"] += r["bytes"]
+        f["n"] += 1
+    name, f = max(fam.items(), key=lambda kv: kv[1]["ms"])
+    return name, f, fam
+
+
+def cpu_baseline(budget_s: float):
+    """Time the CPU oracle on a bounded sample of the same workload (rank 0, N=1)."""
+    sys.path.insert(0, REPO)
+    from oracle import hifigan_ref  # test infrastructure: the baseline being timed, not the product
+    from tts_amd import synthetic
+    from tts_amd.config import HIFIGAN_V1
+
+    cores = len(os.sched_getaffinity(0))
+    threads = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(threads)
+    cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+    sd = synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False)
+    sd = {k: v.float() for k, v in sd.items()}
+    B, T = 1, 256
+    mel = synthetic.mel(B, T, seed=0)
+    with torch.no_grad():
+        hifigan_ref.hifigan_forward(sd, mel[:, :, :8], pad=5, dtype=torch.float32, **cfg)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float32, **cfg)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or n >= 50:
+                break
+    samples = n * B * 256 * (T + 10)
+    return {
+        "value": samples / el,
+        "unit": "samples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} x HifiganGenerator.inference on [1,80,{T}] (oracle/hifigan_ref.py, torch-CPU fp32, "
+                  f"{threads} threads, {el:.1f} s)",
+        "rtf": el / (samples / SAMPLE_RATE),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from tts_amd import synthetic
+    from tts_amd.config import HIFIGAN_V1
+    from tts_amd.vocoder import HifiganGenerator
+
+    cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+    g = HifiganGenerator(**cfg)
+    g.remove_weight_norm()
+    g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False))
+    g.eval()
+    g = g.to(dev)
+    B, T, pad = a.batch, a.frames, g.inference_padding
+    mel = synthetic.mel(B, T, seed=rank).to(dev)
+    g.reserve(B, T)
+    torch.cuda.synchronize(dev)
+
+    for _ in range(a.warmup):
+        g.inference(mel)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = g.inference(mel)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    ms_per_step = el / a.steps * 1e3
+    samples_per_step = B * g.hop_length * (T + 2 * pad)  # per GPU
+    value = world * samples_per_step / (ms_per_step / 1e3)
+    rtf = (ms_per_step / 1e3) / (world * samples_per_step / SAMPLE_RATE)
+
+    comm = None
+    if a.comm and world > 1:
+        from tts_amd.sharding import gather_batch, scatter_batch
+
+        n = B * world
+        full = synthetic.mel(n, T, seed=99).to(dev) if rank == 0 else None
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        c0 = time.perf_counter()
+        shard = scatter_batch(full, n, (80, T), dev)
+        wav = gather_batch(g.inference(shard), n)
+        torch.cuda.synchronize(dev)
+        comm = {"scatter_infer_gather_ms": (time.perf_counter() - c0) * 1e3, "utterances": n}
+
+    # dominant-kernel roofline from one profiled forward (hipEvents per launch)
+    _, rows = g.profile(mel)
+    fam_name, fam, fams = dominant_kernel(rows)
+    per_launch_flops = fam["flops"] / fam["n"]
+    avg_ms = fam["ms"] / fam["n"]
+    achieved = per_launch_flops / (avg_ms / 1e3) / 1e12
+    total_flops = sum(r["flops"] for r in rows)
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            traffic = tj.get("per_launch_bytes", {}).get(fam_name)
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a.cpu_seconds)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
+            "config": {
+                "workload": "HiFiGAN-v1 22.05kHz inference, [32,80,1024] mel per GPU (replicate pad 5), fp32",
+                "model": "HiFiGAN-v1 (hifigan_config.py generator_model_params)",
+                "global_batch": B * world,
+                "seq_len": T,
+                "parallelism": f"dp{world} (utterance sharding, no collectives)",
+            },
+            "rtf": rtf,
+            "model_tflops": total_flops / (ms_per_step / 1e3) / 1e12,
+            "model_frac_fp32_peak": total_flops / (ms_per_step / 1e3) / 1e12 / FP32_PEAK_TFLOPS,
+            "roofline": {
+                "bound": "mfma",
+                "kernel": fam_name,
+                "launches_per_step": fam["n"],
+                "achieved": achieved,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP32_PEAK_TFLOPS,
+                "traffic": traffic,
+                "flops_per_launch": per_launch_flops,
+                "avg_launch_ms": avg_ms,
+            },
+            "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
+            "cpu_baseline": cpu,
+        }
+        if comm:
+            rec["comm"] = comm
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

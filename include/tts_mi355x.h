@@ -1,0 +1,196 @@
+/*
+ * tts_mi355x.h — C-ABI of the MI355X-native mel→waveform path.
+ *
+ * This library replaces, for inference on gfx950, the PyTorch-ATen compute under two
+ * reference modules of Coqui TTS 0.22.0 (paths relative to the reference repo root):
+ *
+ *   HiFiGAN generator  TTS/vocoder/models/hifigan_generator.py
+ *       HifiganGenerator.__init__        :163-234   -> tts_hifigan_create
+ *       HifiganGenerator.forward         :236-265   -> tts_hifigan_forward (pad = 0)
+ *       HifiganGenerator.inference       :267-282   -> tts_hifigan_forward (pad = inference_padding)
+ *       HifiganGenerator.remove_weight_norm :284-291 (weights arrive already folded)
+ *   Glow-TTS decoder   TTS/tts/layers/glow_tts/decoder.py
+ *       Decoder.__init__                 :68-111    -> tts_glow_decoder_create
+ *       Decoder.forward(reverse=True)    :113-137   -> tts_glow_decoder_forward
+ *       Decoder.store_inverse            :139-141   (W^-1 arrives precomputed)
+ *
+ * The reference has no native FFI for this path (it is pure Python over ATen); the Python
+ * binding a maintainer adds is the ctypes stub in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All tensors are fp32, contiguous NCW ([batch][channel][time]) device pointers of the
+ *     device the handle was created on.  Weights are passed as HOST pointers in the
+ *     reference's PyTorch layouts (Conv1d [Cout][Cin][K], ConvTranspose1d [Cin][Cout][K]),
+ *     already weight-norm-folded; the library packs them into kernel layouts once.
+ *   - Every entry point returns TTS_OK (0) or a TTS_ERR_* code; no C++ exception crosses
+ *     the ABI.  tts_last_error() returns the calling thread's last message.
+ *   - forward calls are stream-ordered on the given hipStream_t (NULL = default stream),
+ *     never synchronise (except *_profiled), never allocate after the first call for a given
+ *     (B, T) or smaller (the per-handle workspace grows only).
+ *   - A handle may be used from one host thread at a time; distinct handles are independent.
+ */
+#ifndef TTS_MI355X_H
+#define TTS_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTS_OK 0
+#define TTS_ERR_INVALID 1     /* bad argument / shape (reference: ValueError / assert)      */
+#define TTS_ERR_HIP 2         /* HIP runtime error                                           */
+#define TTS_ERR_UNSUPPORTED 3 /* configuration outside the implemented path                 */
+#define TTS_ERR_OOM 4         /* device allocation failed                                   */
+
+#define TTS_MAX_UPSAMPLES 8
+#define TTS_MAX_KERNELS 4
+#define TTS_MAX_DILATIONS 4
+
+/* ------------------------------------------------------------------------------------ */
+/* Library                                                                               */
+/* ------------------------------------------------------------------------------------ */
+
+/* Last error message of the calling thread ("" if none). */
+const char* tts_last_error(void);
+/* ABI version (major*100 + minor). */
+int tts_abi_version(void);
+/* Target the device code was built for ("gfx950"). */
+const char* tts_build_target(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* HiFiGAN generator                                                                     */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors HifiganGenerator.__init__ arguments (hifigan_generator.py:163-178). */
+typedef struct TtsHifiganCfg {
+  int in_channels;                      /* num_mels (setup_generator, vocoder/models/__init__.py:41) */
+  int out_channels;                     /* 1 */
+  int resblock_type;                    /* 1 = ResBlock1 (:18-105), 2 = ResBlock2 (:108-159) */
+  int num_kernels;                      /* len(resblock_kernel_sizes) */
+  int resblock_kernel_sizes[TTS_MAX_KERNELS];
+  int num_dilations;                    /* len(resblock_dilation_sizes[j]); 3 (type 1) or 2 (type 2) */
+  int resblock_dilation_sizes[TTS_MAX_KERNELS][TTS_MAX_DILATIONS];
+  int num_upsamples;                    /* len(upsample_factors) */
+  int upsample_factors[TTS_MAX_UPSAMPLES];
+  int upsample_kernel_sizes[TTS_MAX_UPSAMPLES];
+  int upsample_initial_channel;
+  int inference_padding;                /* default 5 (:173) */
+  int cond_channels;                    /* 0 = no cond_layer (:227-228) */
+  int conv_post_bias;                   /* default 1 (:177) */
+} TtsHifiganCfg;
+
+/* Number of host weight tensors create() expects, and the element count of tensor idx.
+ * Order (state_dict order of the reference module after remove_weight_norm):
+ *   conv_pre.weight [C0][in][7], conv_pre.bias [C0]
+ *   for i < num_upsamples:  ups.i.weight [C_i][C_i/2][k_i], ups.i.bias [C_i/2]
+ *   for r < num_upsamples*num_kernels (resblocks.r):
+ *       type 1: convs1.m.weight/bias for m < 3, then convs2.m.weight/bias for m < 3
+ *       type 2: convs.m.weight/bias for m < num_dilations
+ *   conv_post.weight [out][C_last][7], conv_post.bias [out] (only if conv_post_bias)
+ *   cond_layer.weight [C0][cond][1], cond_layer.bias [C0]  (only if cond_channels > 0)
+ * with C0 = upsample_initial_channel, C_i = C0 >> i. */
+int tts_hifigan_num_weights(const TtsHifiganCfg* cfg);
+int64_t tts_hifigan_weight_numel(const TtsHifiganCfg* cfg, int idx);
+
+/* Build a generator on HIP device `device`: validates cfg, packs + uploads weights. */
+int tts_hifigan_create(const TtsHifiganCfg* cfg, const float* const* host_weights, int device,
+                       void** handle);
+int tts_hifigan_destroy(void* handle);
+
+/* Output samples per batch item: prod(upsample_factors) * (T + 2*pad). */
+int64_t tts_hifigan_output_length(const void* handle, int T, int pad);
+/* Workspace the handle needs for (B, T, pad), and an explicit pre-allocation. */
+int64_t tts_hifigan_workspace_bytes(const void* handle, int B, int T, int pad);
+int tts_hifigan_reserve(void* handle, int B, int T, int pad);
+
+/* wav[B][out][hop*(T+2*pad)] = G(replicate_pad(mel[B][C][T], pad)).  pad = 0 is
+ * HifiganGenerator.forward, pad = inference_padding is .inference (hifigan_generator.py:281).
+ * d_g ([B][cond_channels], may be NULL when cond_channels == 0) is the global conditioning
+ * vector (the reference's g[B][cond][1], :250-251). */
+int tts_hifigan_forward(void* handle, const float* d_mel, int B, int C, int T, int pad,
+                        const float* d_g, float* d_wav, void* hip_stream);
+
+/* Same computation, with a hipEvent pair around every kernel launch.  Synchronises the
+ * stream before returning.  records[i] describes launch i in issue order. */
+typedef struct TtsLaunchRecord {
+  char name[48];    /* kernel family, e.g. "mrf_conv_k11_c128" */
+  double flops;     /* algorithmic FLOPs of this launch (2*MACs, no padding waste) */
+  double bytes;     /* compulsory HBM bytes of this launch (inputs + weights + outputs) */
+  float ms;         /* measured duration */
+} TtsLaunchRecord;
+int tts_hifigan_forward_profiled(void* handle, const float* d_mel, int B, int C, int T, int pad,
+                                 const float* d_g, float* d_wav, void* hip_stream,
+                                 TtsLaunchRecord* records, int max_records, int* n_records);
+
+/* ------------------------------------------------------------------------------------ */
+/* Glow-TTS decoder flow (reverse)                                                        */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors Decoder.__init__ (decoder.py:68-81). */
+typedef struct TtsGlowDecoderCfg {
+  int in_channels;         /* 80 (out_channels of GlowTTS) */
+  int hidden_channels;     /* 192 (hidden_channels_dec) */
+  int kernel_size;         /* 5 */
+  int dilation_rate;       /* 1 */
+  int num_flow_blocks;     /* 12 */
+  int num_coupling_layers; /* 4 */
+  int num_splits;          /* 4 */
+  int num_squeeze;         /* 2 */
+  int sigmoid_scale;       /* 0 */
+  int c_in_channels;       /* 0 (speaker conditioning not implemented: must be 0) */
+} TtsGlowDecoderCfg;
+
+/* Host weight order, per flow block b < num_flow_blocks (flows 3b, 3b+1, 3b+2):
+ *   actnorm.logs [C2], actnorm.bias [C2]                          (C2 = in*num_squeeze)
+ *   invconv.weight_inv [S][S]  (torch.inverse(weight), glow.py:139-141)
+ *   coupling.start.weight [H][C2/2] (weight-norm folded), coupling.start.bias [H]
+ *   for l < L: wn.in_layers.l.weight [2H][H][k], wn.in_layers.l.bias [2H]
+ *              wn.res_skip_layers.l.weight [l<L-1 ? 2H : H][H], bias
+ *   coupling.end.weight [C2][H], coupling.end.bias [C2] */
+int tts_glow_decoder_num_weights(const TtsGlowDecoderCfg* cfg);
+int64_t tts_glow_decoder_weight_numel(const TtsGlowDecoderCfg* cfg, int idx);
+int tts_glow_decoder_create(const TtsGlowDecoderCfg* cfg, const float* const* host_weights,
+                            int device, void** handle);
+int tts_glow_decoder_destroy(void* handle);
+/* y[B][C][T'] = Decoder.forward(x, x_mask, reverse=reverse)[0] with T' = T rounded down to a
+ * multiple of num_squeeze (decoder.py:19); d_mask is [B][1][T] (0/1).  Only reverse = 1 is
+ * implemented (the inference direction, glow_tts.py:363). */
+int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, int B, int C,
+                             int T, int reverse, float* d_y, void* hip_stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Single-op entry points (test / tuning surface).  These pack the host weights into a     */
+/* temporary device buffer on every call and synchronise; they are not the hot path.        */
+/* ------------------------------------------------------------------------------------ */
+
+/* y = epilogue(conv1d(act_in(x_padded), w) + b), "same" conv: pad = dil*(K-1)/2.
+ * x_padded[t] = x[clamp(t - rep_pad, 0, Tin-1)] for t in [0, Tin + 2*rep_pad).
+ * act_in / act_out = leaky_relu with the given slope (1.0 = identity).
+ * Epilogue: v = act_out(acc + b) + (res ? res : 0);
+ *   zmode 0: y = v;  1: z = v;  2: z = z + v;  3: z = (z + v) / zdiv. */
+typedef struct TtsConv1dDesc {
+  int B, Cin, Cout, Tin, K, dil, rep_pad;
+  float in_slope, out_slope;
+  int zmode;
+  float zdiv;
+} TtsConv1dDesc;
+int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
+                  const float* d_res, float* d_y, float* d_z, void* hip_stream);
+
+/* y = conv_transpose1d(act_in(x), w[Cin][Cout][K], b, stride, padding=(K-stride)/2);
+ * requires K == 2*stride (every HiFiGAN config). */
+int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
+                            const float* h_b, int Cout, int K, int stride, float in_slope,
+                            float* d_y, void* hip_stream);
+
+/* y[B][1][T] = tanh(conv1d(leaky_relu(z, in_slope), w[1][Cin][7], b, pad 3)). */
+int tts_op_conv_post(const float* d_z, int B, int Cin, int T, const float* h_w, const float* h_b,
+                     float in_slope, float* d_y, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TTS_MI355X_H */

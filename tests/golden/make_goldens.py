@@ -1,0 +1,172 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE modules.
+
+Run in the development container only (it imports /root/reference, which does not exist on
+the GPU box):   python tests/golden/make_goldens.py
+
+Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
+but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
+(absent), so those two packages are pre-registered as bare namespace packages.
+
+Weights are NOT stored: they are regenerated from the seed with tts_amd.synthetic (a
+deterministic numpy stream), and each fixture records its config and seed.  Every fixture
+holds the reference's fp32 CPU output and the same module run in fp64 (``.double()``), the
+accuracy anchor for the tolerance gates.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("TTS_REFERENCE", "/root/reference")
+sys.path.insert(0, os.path.join(REPO, "tts-3_amd"))
+
+from tts_amd import synthetic  # noqa: E402  (numpy/torch only; no native library needed)
+
+
+def import_reference():
+    sys.path.insert(0, REF)
+    import TTS  # noqa: F401
+
+    for name, sub in [
+        ("TTS.tts", "TTS/tts"),
+        ("TTS.tts.layers", "TTS/tts/layers"),
+        ("TTS.vocoder", "TTS/vocoder"),
+        ("TTS.vocoder.models", "TTS/vocoder/models"),
+    ]:
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            m.__path__ = [os.path.join(REF, sub)]
+            sys.modules[name] = m
+    from TTS.vocoder.models.hifigan_generator import HifiganGenerator
+    from TTS.tts.layers.glow_tts.decoder import Decoder
+
+    return HifiganGenerator, Decoder
+
+
+def hifigan_case(HifiganGenerator, name, cfg, seed, B, T, mel_seed, stage_B=None, stage_T=None, with_forward=True):
+    torch.manual_seed(0)
+    ctor = {k: v for k, v in cfg.items() if k != "seed"}
+    ref = HifiganGenerator(**ctor)
+    sd = synthetic.hifigan_state_dict(**cfg, seed=seed, weight_norm=True)
+    ref.load_state_dict(sd)
+    ref.eval()
+    if cfg.get("conv_pre_weight_norm", True):
+        ref.remove_weight_norm()  # eval load (gan.py:249-252); VITS keeps its parametrizations
+    mel = synthetic.mel(B, T, channels=cfg["in_channels"], seed=mel_seed)
+    g = None
+    extra = {}
+    if cfg.get("cond_channels", 0) > 0:
+        gen = torch.Generator().manual_seed(mel_seed + 1)
+        g = torch.randn(B, cfg["cond_channels"], 1, generator=gen)
+        extra["g"] = g.numpy()
+
+    def run(model, x, gg, pad):
+        with torch.no_grad():
+            if pad:
+                x = torch.nn.functional.pad(x, (pad, pad), "replicate")
+            return model.forward(x, gg) if gg is not None else model.forward(x)
+
+    pad = cfg.get("inference_padding", 5)
+    with torch.no_grad():
+        out32 = ref.inference(mel) if g is None else run(ref, mel, g, pad)
+    ref64 = ref.double()
+    out64 = run(ref64, mel.double(), None if g is None else g.double(), pad)
+    ref.float()
+    arrays = dict(mel=mel.numpy(), out_ref_fp32=out32.numpy(), out_ref_fp64=out64.numpy(), **extra)
+    if with_forward:  # forward() path: no inference padding
+        arrays["fwd_ref_fp64"] = run(ref64.double(), mel.double(), None if g is None else g.double(), 0).numpy()
+        ref.float()
+    if stage_B:
+        smel = synthetic.mel(stage_B, stage_T, channels=cfg["in_channels"], seed=mel_seed + 7)
+        hooks, caps = [], {}
+        ref64 = ref.double()
+        hooks.append(ref64.conv_pre.register_forward_hook(lambda m, i, o: caps.__setitem__("conv_pre", o)))
+        for i, u in enumerate(ref64.ups):
+            hooks.append(u.register_forward_hook(lambda m, inp, o, i=i: caps.__setitem__(f"ups.{i}", o)))
+        with torch.no_grad():
+            ref64.inference(smel.double())
+        for h in hooks:
+            h.remove()
+        ref.float()
+        arrays["stage_mel"] = smel.numpy()
+        for k, v in caps.items():
+            arrays["stage_" + k] = v.float().numpy()
+    meta = dict(kind="hifigan", config=cfg, seed=seed, mel_seed=mel_seed, B=B, T=T, pad=pad,
+                stage_B=stage_B, stage_T=stage_T)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: out {tuple(out32.shape)} std {out32.std():.4f} "
+          f"max|fp32-fp64| {np.abs(out32.numpy() - out64.numpy()).max():.2e}")
+
+
+def glow_case(Decoder, name, cfg, seed, B, T, lengths, x_seed):
+    torch.manual_seed(0)
+    ref = Decoder(
+        in_channels=cfg["in_channels"], hidden_channels=cfg["hidden_channels"], kernel_size=cfg["kernel_size"],
+        dilation_rate=cfg["dilation_rate"], num_flow_blocks=cfg["num_flow_blocks"],
+        num_coupling_layers=cfg["num_coupling_layers"], dropout_p=0.05, num_splits=cfg["num_splits"],
+        num_squeeze=cfg["num_squeeze"], sigmoid_scale=False, c_in_channels=0,
+    )
+    sd = synthetic.glow_decoder_state_dict(**cfg, seed=seed)
+    ref.load_state_dict(sd)
+    ref.eval()
+    ref.store_inverse()  # glow_tts.py:519-520, :529 (eval load)
+    gen = torch.Generator().manual_seed(x_seed)
+    x = torch.randn(B, cfg["in_channels"], T, generator=gen)
+    lengths_t = torch.tensor(lengths)
+    mask = (torch.arange(T)[None, :] < lengths_t[:, None]).float().unsqueeze(1)
+    with torch.no_grad():
+        y32, _ = ref(x, mask, reverse=True)
+        ref64 = ref.double()
+        y64, _ = ref64(x.double(), mask.double(), reverse=True)
+        # round trip through the reference's own forward direction
+        z64, logdet = ref64(y64, mask.double()[:, :, : y64.size(2)], reverse=False)
+    meta = dict(kind="glow", config=cfg, seed=seed, x_seed=x_seed, B=B, T=T, lengths=lengths)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), x=x.numpy(), mask=mask.numpy(), out_ref_fp32=y32.numpy(),
+                        out_ref_fp64=y64.numpy(), roundtrip_fp64=z64.numpy(), logdet_fp64=logdet.numpy())
+    print(f"wrote {path}: out {tuple(y32.shape)} std {y32.std():.4f} "
+          f"max|fp32-fp64| {np.abs(y32.numpy() - y64.numpy()).max():.2e}")
+
+
+def main():
+    HifiganGenerator, Decoder = import_reference()
+    v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
+              resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+              upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=512, upsample_factors=[8, 8, 2, 2],
+              inference_padding=5)
+    # G1: HiFiGAN-v1 (the benchmark architecture), full output + per-stage intermediates
+    hifigan_case(HifiganGenerator, "hifigan_v1_b2_t32", v1, seed=1234, B=2, T=32, mel_seed=0,
+                 stage_B=1, stage_T=4)
+    # G1b: single frame (smallest input the reference accepts with inference padding)
+    hifigan_case(HifiganGenerator, "hifigan_v1_b1_t1", v1, seed=1234, B=1, T=1, mel_seed=3, with_forward=False)
+    # G2: HiFiGAN-v3 topology (ResBlock2, dilations up to 12, x4 upsample) at reduced width
+    v3s = dict(in_channels=80, out_channels=1, resblock_type="2",
+               resblock_dilation_sizes=[[1, 2], [2, 6], [3, 12]], resblock_kernel_sizes=[3, 5, 7],
+               upsample_kernel_sizes=[16, 16, 8], upsample_initial_channel=128, upsample_factors=[8, 8, 4],
+               inference_padding=5)
+    hifigan_case(HifiganGenerator, "hifigan_small_rb2_b2_t16", v3s, seed=77, B=2, T=16, mel_seed=5)
+    # G4: VITS-style decoder (vits.py:704-718): in 192, cond, no conv_post bias, no padding, no WN
+    vits = dict(in_channels=192, out_channels=1, resblock_type="1",
+                resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+                upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=128, upsample_factors=[8, 8, 2, 2],
+                inference_padding=0, cond_channels=16, conv_pre_weight_norm=False, conv_post_weight_norm=False,
+                conv_post_bias=False)
+    hifigan_case(HifiganGenerator, "hifigan_vits_cond_b2_t12", vits, seed=99, B=2, T=12, mel_seed=11,
+                 with_forward=False)
+    # G3: Glow-TTS decoder reverse, LJSpeech config, ragged mask with an odd length
+    glow = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+                num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    glow_case(Decoder, "glow_decoder_b2_t64", glow, seed=4321, B=2, T=64, lengths=[64, 41], x_seed=21)
+    glow_case(Decoder, "glow_decoder_b3_t33", glow, seed=4322, B=3, T=33, lengths=[33, 20, 1], x_seed=22)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+"""C-ABI surface and host logic, no GPU: the library loads, exports every symbol declared in
+include/tts_mi355x.h, validates configurations with the documented status codes, and the
+Python drop-ins accept reference state_dicts and fail loudly off-device."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from _util import GOLDEN, hifigan_ctor
+from oracle import glow_ref, hifigan_ref
+from tts_amd import _native as N
+from tts_amd import synthetic
+from tts_amd.config import HIFIGAN_V1
+from tts_amd.tts import Decoder
+from tts_amd.vocoder import GAN, HifiganGenerator, setup_generator
+
+HEADER = os.path.join(os.path.dirname(GOLDEN), "..", "include", "tts_mi355x.h")
+V1 = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tts_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.lib()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"{n} not exported"
+        assert n in N.SIGNATURES, f"{n} has no ctypes signature"
+    assert set(N.SIGNATURES) == set(names)
+
+
+def test_version_and_target():
+    assert N.lib().tts_abi_version() == 100
+    assert N.lib().tts_build_target() == b"gfx950"
+    assert N.lib().tts_last_error() == b""
+
+
+def _cfg(**over):
+    g = HifiganGenerator(**{**V1, **over})
+    return g._cfg
+
+
+def test_hifigan_weight_inventory_matches_module():
+    g = HifiganGenerator(**V1)
+    ws = g._weight_list()
+    n = N.lib().tts_hifigan_num_weights(ctypes.byref(g._cfg))
+    assert n == len(ws) == 2 + 8 + 4 * 3 * 12 + 2
+    for i, w in enumerate(ws):
+        assert N.lib().tts_hifigan_weight_numel(ctypes.byref(g._cfg), i) == w.size
+    assert N.lib().tts_hifigan_weight_numel(ctypes.byref(g._cfg), n) == -1
+    assert sum(w.size for w in ws) == 13926017  # HiFiGAN-v1 after weight-norm removal
+
+
+@pytest.mark.parametrize(
+    "over,code,msg",
+    [
+        (dict(upsample_kernel_sizes=[16, 15, 4, 4]), N.TTS_ERR_UNSUPPORTED, "2*factor"),
+        (dict(upsample_factors=[8, 8, 3, 2], upsample_kernel_sizes=[16, 16, 6, 4]), N.TTS_ERR_UNSUPPORTED, "2, 4 or 8"),
+        (dict(resblock_kernel_sizes=[3, 9, 11]), N.TTS_ERR_UNSUPPORTED, "kernel size"),
+        (dict(resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 40]]), N.TTS_ERR_UNSUPPORTED, "dilation"),
+    ],
+)
+def test_hifigan_config_validation(over, code, msg):
+    with pytest.raises(N.NativeError) as e:
+        HifiganGenerator(**{**V1, **over})
+    assert e.value.code == code
+    assert msg in str(e.value)
+
+
+def test_out_channels_unsupported_status():
+    with pytest.raises(N.NativeError) as e:
+        HifiganGenerator(**{**V1, "out_channels": 4})
+    assert e.value.code == N.TTS_ERR_UNSUPPORTED
+
+
+def test_state_dict_keys_match_reference_checkpoints():
+    sd = synthetic.hifigan_state_dict(seed=1)  # the same dict make_goldens.py loads into the reference
+    g = HifiganGenerator(**V1)
+    g.load_state_dict(sd)  # strict
+    assert list(g.state_dict().keys()) == list(sd.keys())
+
+
+def test_fold_matches_reference_remove_weight_norm():
+    sd = synthetic.hifigan_state_dict(seed=2)
+    g = HifiganGenerator(**V1)
+    g.load_state_dict(sd)
+    before = g._weight_list()
+    g.remove_weight_norm()
+    after = g._weight_list()
+    folded = hifigan_ref.fold_weight_norm(sd, torch.float32)
+    assert np.array_equal(before[0], folded["conv_pre.weight"].numpy())
+    for a, b in zip(before, after):
+        assert np.array_equal(a, b)
+    assert "conv_pre.weight" in g.state_dict()
+
+
+def test_cpu_module_refuses_to_run():
+    g = HifiganGenerator(**V1)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        g.inference(torch.zeros(1, 80, 4))
+
+
+def test_setup_generator_and_gan_surface(tmp_path):
+    cfg = {"generator_model": "hifigan_generator", "audio": {"num_mels": 80},
+           "generator_model_params": dict(HIFIGAN_V1)}
+    gan = GAN.init_from_config(cfg)
+    assert isinstance(gan.model_g, HifiganGenerator)
+    sd = synthetic.hifigan_state_dict(seed=5)
+    path = tmp_path / "ckpt.pth"
+    torch.save({"model": {"model_g." + k: v for k, v in sd.items()}}, path)
+    gan.load_checkpoint(cfg, str(path), eval=True)
+    assert gan.model_d is None
+    w = gan.model_g._weight_list()
+    assert np.array_equal(w[0], hifigan_ref.fold_weight_norm(sd, torch.float32)["conv_pre.weight"].numpy())
+    with pytest.raises(NotImplementedError):
+        setup_generator({**cfg, "generator_model": "melgan_generator"})
+
+
+def test_hifigan_generator_load_checkpoint(tmp_path):
+    sd = synthetic.hifigan_state_dict(seed=6)
+    path = tmp_path / "g.pth"
+    torch.save({"model": sd}, path)
+    g = HifiganGenerator(**V1)
+    g.load_checkpoint({}, str(path), eval=True)
+    assert not g.training
+    assert not any(".parametrizations." in k for k in g.state_dict())
+
+
+def test_glow_decoder_surface():
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4)
+    d = Decoder(**cfg, dropout_p=0.05, num_splits=4, num_squeeze=2)
+    sd = synthetic.glow_decoder_state_dict(seed=7)
+    d.load_state_dict(sd)  # strict: reference key set
+    d.eval()
+    d.store_inverse()
+    ws = d._weight_list()
+    n = N.lib().tts_glow_decoder_num_weights(ctypes.byref(d._cfg))
+    assert n == len(ws) == 12 * (5 + 4 * 4 + 2)
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_decoder_weight_numel(ctypes.byref(d._cfg), i) == w.size
+    # W^-1 identical to the oracle's (reference store_inverse semantics)
+    winv = torch.inverse(d.flows[1].weight.detach().float())
+    wf = sd["flows.1.weight"].float()
+    assert torch.equal(winv, torch.inverse(wf.t().contiguous().t()))
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), reverse=True)
+    with pytest.raises(NotImplementedError):
+        d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), reverse=False)
+
+
+def test_glow_config_validation():
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 3, 2, 0, 0)
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    assert b"num_splits" in N.lib().tts_last_error()
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+
+
+def test_null_arguments_return_invalid():
+    lib = N.lib()
+    assert lib.tts_hifigan_create(None, None, 0, None) == N.TTS_ERR_INVALID
+    assert lib.tts_hifigan_forward(None, None, 1, 80, 4, 0, None, None, None) == N.TTS_ERR_INVALID
+    assert b"NULL" in lib.tts_last_error()
+    assert lib.tts_hifigan_destroy(None) == N.TTS_OK
+    assert lib.tts_glow_decoder_destroy(None) == N.TTS_OK

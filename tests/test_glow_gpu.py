@@ -1,0 +1,61 @@
+"""Glow-TTS decoder (reverse flow) parity on MI355X vs the reference goldens and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close_fp32, goldens, max_abs
+from oracle import glow_ref
+from tts_amd import synthetic
+from tts_amd.tts import Decoder
+
+pytestmark = pytest.mark.gpu
+GLOW = goldens("glow")
+# the reference's own fp32-vs-fp64 error on this flow is 2.9e-6 (12 flows, exp() of scales)
+GLOW_MAX_ABS = 1e-4
+GLOW_REL_RMS = 2e-5
+
+
+def build(cfg, seed, device):
+    d = Decoder(cfg["in_channels"], cfg["hidden_channels"], cfg["kernel_size"], cfg["dilation_rate"],
+                cfg["num_flow_blocks"], cfg["num_coupling_layers"], dropout_p=0.05,
+                num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"])
+    d.load_state_dict(synthetic.glow_decoder_state_dict(**cfg, seed=seed))
+    d.eval()
+    d.store_inverse()
+    return d.to(device)
+
+
+@pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
+def test_glow_reverse_vs_reference(cuda_device, name, meta, arr):
+    d = build(meta["config"], meta["seed"], cuda_device)
+    x = torch.from_numpy(arr["x"]).to(cuda_device)
+    m = torch.from_numpy(arr["mask"]).to(cuda_device)
+    y, logdet = d(x, m, reverse=True)
+    assert logdet is None
+    assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, GLOW_MAX_ABS, GLOW_REL_RMS)
+
+
+@pytest.mark.parametrize("B,T,lengths", [(1, 2, [2]), (2, 7, [7, 3]), (4, 400, [400, 399, 200, 1])])
+def test_glow_reverse_vs_oracle(cuda_device, B, T, lengths):
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    d = build(cfg, 99, cuda_device)
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(B, 80, T, generator=g)
+    m = (torch.arange(T)[None] < torch.tensor(lengths)[:, None]).float().unsqueeze(1)
+    y, _ = d(x.to(cuda_device), m.to(cuda_device), reverse=True)
+    ref = glow_ref.glow_decoder_reverse(synthetic.glow_decoder_state_dict(**cfg, seed=99), x, m, **cfg)
+    assert_close_fp32(y.cpu(), ref, f"glow B={B} T={T}", GLOW_MAX_ABS, GLOW_REL_RMS)
+
+
+def test_glow_batch_invariance(cuda_device):
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    d = build(cfg, 5, cuda_device)
+    x = torch.randn(16, 80, 768, generator=torch.Generator().manual_seed(1)).to(cuda_device)
+    m = torch.ones(16, 1, 768, device=cuda_device)
+    y, _ = d(x, m, reverse=True)
+    y1, _ = d(x[3:4], m[3:4], reverse=True)
+    assert torch.equal(y[3], y1[0])
+    y2, _ = d(x, m, reverse=True)
+    assert torch.equal(y, y2)

@@ -1,0 +1,222 @@
+"""HiFiGAN parity on MI355X through the C-ABI (libtts_mi355x.so).
+
+* single kernels (tts_op_*) vs torch.nn.functional fp64 on the CPU, over the shapes of
+  HiFiGAN v1/v3, ragged channel counts, edge lengths, every epilogue mode;
+* the whole generator vs the reference's own outputs (tests/golden, fp64 anchor);
+* at the benchmark size (B=32 x 1024 frames) the size-independent properties: finite,
+  |y| <= 1, batch-invariance (each utterance bit-identical to running it alone),
+  run-to-run determinism, and one utterance vs the fp32 CPU oracle.
+
+fp32 gates: max|d| <= 1e-4 and rel-RMS <= 1e-5 against the fp64 reference.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from _util import assert_close_fp32, goldens, hifigan_ctor, max_abs, rel_rms
+from oracle import hifigan_ref
+from tts_amd import _native as N
+from tts_amd import synthetic
+from tts_amd.config import HIFIGAN_V1
+from tts_amd.vocoder import HifiganGenerator
+
+pytestmark = pytest.mark.gpu
+V1 = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+
+
+def _rng(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+# ----------------------------------------------------------------------------- conv1d
+CONV_CASES = [
+    # B, Cin, Cout, T, K, dil, rep, in_slope, out_slope, res, zmode
+    (2, 80, 512, 37, 7, 1, 5, 1.0, 1.0, False, 0),     # conv_pre with replicate padding
+    (2, 256, 256, 300, 11, 5, 0, 0.1, 0.1, False, 0),  # MRF convs1, stage 1
+    (1, 256, 256, 129, 3, 1, 0, 1.0, 1.0, True, 0),    # convs2 + residual
+    (1, 128, 128, 1000, 7, 3, 0, 0.1, 0.1, False, 0),
+    (2, 64, 64, 777, 3, 1, 0, 1.0, 1.0, True, 1),      # z init
+    (1, 64, 64, 600, 11, 1, 0, 1.0, 1.0, True, 2),     # z accumulate
+    (1, 32, 32, 1100, 11, 5, 0, 1.0, 1.0, True, 3),    # z final (/3)
+    (3, 33, 17, 50, 5, 2, 0, 0.1, 1.0, False, 0),      # ragged channels
+    (1, 24, 40, 97, 7, 12, 0, 0.1, 1.0, True, 0),      # HiFiGAN-v3 dilation 12 (wide halo)
+    (2, 192, 384, 61, 5, 1, 0, 1.0, 1.0, False, 0),    # Glow WN in_layer
+    (1, 80, 192, 33, 1, 1, 0, 1.0, 1.0, False, 0),     # 1x1
+    (1, 16, 16, 1, 11, 5, 0, 0.1, 0.1, False, 0),      # single frame
+    (1, 80, 512, 1, 7, 1, 5, 1.0, 1.0, False, 0),      # single mel frame + replicate pad
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{i}" for i in range(len(CONV_CASES))])
+def test_op_conv1d(cuda_device, case):
+    B, Cin, Cout, T, K, dil, rep, s_in, s_out, use_res, zmode = case
+    g = _rng(hash(case) & 0xFFFF)
+    x = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g) * 0.1
+    To = T + 2 * rep
+    res = torch.randn(B, Cout, To, generator=g) if use_res else None
+    z0 = torch.randn(B, Cout, To, generator=g)
+    # fp64 reference
+    xp = F.pad(x.double(), (rep, rep), "replicate") if rep else x.double()
+    v = F.conv1d(F.leaky_relu(xp, s_in), w.double(), b.double(), dilation=dil, padding=dil * (K - 1) // 2)
+    v = F.leaky_relu(v, s_out)
+    if res is not None:
+        v = v + res.double()
+    ref = {0: v, 1: v, 2: z0.double() + v, 3: (z0.double() + v) / 3.0}[zmode]
+    d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, rep, s_in, s_out, zmode, 3.0)
+    xd = x.to(cuda_device)
+    resd = res.to(cuda_device) if res is not None else None
+    y = torch.full((B, Cout, To), float("nan"), device=cuda_device)
+    z = z0.to(cuda_device)
+    wn, bn = w.numpy().copy(), b.numpy().copy()
+    N.call("tts_op_conv1d", ctypes.byref(d), N.ptr(xd), N.ptr(wn), N.ptr(bn), N.ptr(resd), N.ptr(y), N.ptr(z),
+           N.stream_ptr(cuda_device))
+    out = y if zmode == 0 else z
+    assert_close_fp32(out.cpu(), ref, f"conv1d {case}")
+
+
+# ----------------------------------------------------------------------------- conv_transpose1d
+CONVT_CASES = [
+    # B, Cin, Cout, T, U
+    (2, 512, 256, 37, 8),
+    (1, 256, 128, 100, 8),
+    (2, 128, 64, 129, 2),
+    (1, 64, 32, 300, 2),
+    (1, 256, 128, 1, 8),
+    (2, 64, 32, 50, 4),
+    (1, 48, 24, 17, 2),   # ragged
+    (3, 40, 20, 9, 8),    # ragged
+]
+
+
+@pytest.mark.parametrize("case", CONVT_CASES, ids=[f"t{i}" for i in range(len(CONVT_CASES))])
+def test_op_conv_transpose1d(cuda_device, case):
+    B, Cin, Cout, T, U = case
+    K = 2 * U
+    g = _rng(1000 + T)
+    x = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(Cin, Cout, K, generator=g) / np.sqrt(Cin * 2)
+    b = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv_transpose1d(F.leaky_relu(x.double(), 0.1), w.double(), b.double(), stride=U, padding=(K - U) // 2)
+    y = torch.full((B, Cout, U * T), float("nan"), device=cuda_device)
+    wn, bn = w.numpy().copy(), b.numpy().copy()
+    N.call("tts_op_conv_transpose1d", N.ptr(x.to(cuda_device)), B, Cin, T, N.ptr(wn), N.ptr(bn), Cout, K, U, 0.1,
+           N.ptr(y), N.stream_ptr(cuda_device))
+    assert_close_fp32(y.cpu(), ref, f"convT {case}")
+
+
+@pytest.mark.parametrize("B,Cin,T", [(2, 32, 1000), (1, 32, 1), (3, 8, 513)])
+def test_op_conv_post(cuda_device, B, Cin, T):
+    g = _rng(T)
+    z = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(1, Cin, 7, generator=g) / np.sqrt(Cin * 7)
+    b = torch.randn(1, generator=g) * 0.1
+    ref = torch.tanh(F.conv1d(F.leaky_relu(z.double(), 0.01), w.double(), b.double(), padding=3))
+    y = torch.full((B, 1, T), float("nan"), device=cuda_device)
+    wn, bn = w.numpy().copy(), b.numpy().copy()
+    N.call("tts_op_conv_post", N.ptr(z.to(cuda_device)), B, Cin, T, N.ptr(wn), N.ptr(bn), 0.01, N.ptr(y),
+           N.stream_ptr(cuda_device))
+    assert_close_fp32(y.cpu(), ref, "conv_post")
+
+
+# ----------------------------------------------------------------------------- whole generator
+HIFI = goldens("hifigan")
+
+
+def build(cfg, seed, device):
+    g = HifiganGenerator(**hifigan_ctor(cfg))
+    g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=seed, weight_norm=True))
+    g.eval()
+    if cfg.get("conv_pre_weight_norm", True):
+        g.remove_weight_norm()
+    return g.to(device)
+
+
+@pytest.mark.parametrize("name,meta,arr", HIFI, ids=[h[0] for h in HIFI])
+def test_generator_vs_reference_goldens(cuda_device, name, meta, arr):
+    cfg = meta["config"]
+    g = build(cfg, meta["seed"], cuda_device)
+    mel = torch.from_numpy(arr["mel"]).to(cuda_device)
+    gv = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
+    out = g.inference(mel, gv) if gv is not None else g.inference(mel)
+    assert_close_fp32(out.cpu(), arr["out_ref_fp64"], f"{name} inference")
+    # and as close to the reference fp32 CPU forward as that forward is to fp64
+    assert max_abs(out.cpu().numpy(), arr["out_ref_fp32"]) < 1e-4
+    if "fwd_ref_fp64" in arr:
+        fwd = g(mel, gv) if gv is not None else g(mel)
+        assert_close_fp32(fwd.cpu(), arr["fwd_ref_fp64"], f"{name} forward")
+
+
+def test_generator_stage_parity(cuda_device):
+    """conv_pre / ups outputs via the op entry points on the reference's own intermediates."""
+    name, meta, arr = [h for h in HIFI if "stage_conv_pre" in h[2]][0]
+    cfg = meta["config"]
+    sd = hifigan_ref.fold_weight_norm(synthetic.hifigan_state_dict(**cfg, seed=meta["seed"]), torch.float32)
+    mel = torch.from_numpy(arr["stage_mel"])
+    B, C, T = mel.shape
+    P = meta["pad"]
+    d = N.TtsConv1dDesc(B, C, 512, T, 7, 1, P, 1.0, 1.0, 0, 1.0)
+    y = torch.empty(B, 512, T + 2 * P, device=cuda_device)
+    w, b = sd["conv_pre.weight"].float().numpy().copy(), sd["conv_pre.bias"].float().numpy().copy()
+    N.call("tts_op_conv1d", ctypes.byref(d), N.ptr(mel.to(cuda_device)), N.ptr(w), N.ptr(b), None, N.ptr(y), None,
+           N.stream_ptr(cuda_device))
+    assert_close_fp32(y.cpu(), arr["stage_conv_pre"], "conv_pre stage", max_abs_tol=1e-5)
+
+
+def test_generator_edge_lengths_vs_oracle(cuda_device):
+    sd = synthetic.hifigan_state_dict(seed=31, weight_norm=False)
+    g = HifiganGenerator(**V1)
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    for B, T, pad in [(1, 1, 0), (2, 3, 0), (1, 2, 5), (3, 67, 5)]:
+        mel = synthetic.mel(B, T, seed=T)
+        out = g._run(mel.to(cuda_device), pad, None)
+        ref = hifigan_ref.hifigan_forward(sd, mel, pad=pad, dtype=torch.float64, **V1)
+        assert_close_fp32(out.cpu(), ref, f"B={B} T={T} pad={pad}")
+
+
+def test_input_validation(cuda_device):
+    g = HifiganGenerator(**V1).to(cuda_device)
+    with pytest.raises(ValueError):
+        g.inference(torch.zeros(1, 81, 4, device=cuda_device))
+    with pytest.raises(ValueError):
+        g.inference(torch.zeros(80, 4, device=cuda_device))
+
+
+def test_profiled_forward_records(cuda_device):
+    g = build(dict(V1, inference_padding=5), 1234, cuda_device)
+    mel = synthetic.mel(2, 16).to(cuda_device)
+    out, rows = g.profile(mel)
+    assert len(rows) == 1 + 4 + 4 * 3 * 6 + 1  # conv_pre, ups, 72 MRF convs, conv_post
+    assert all(r["ms"] > 0 for r in rows)
+    flops = sum(r["flops"] for r in rows)
+    # 614.1 MFLOP per padded frame, minus the conv zero-padding waste at T'=26
+    assert 0.9 * 614.1e6 * 2 * 26 < flops <= 614.2e6 * 2 * 26
+    assert torch.equal(out, g.inference(mel))
+
+
+@pytest.mark.slow
+def test_benchmark_size_properties(cuda_device):
+    """Config 2 of BASELINE.json: B=32 x 1024 frames, HiFiGAN-v1, fp32."""
+    sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
+    g = HifiganGenerator(**V1)
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    mel = synthetic.mel(32, 1024, seed=0).to(cuda_device)
+    out = g.inference(mel)
+    assert out.shape == (32, 1, 256 * 1034)
+    assert torch.isfinite(out).all() and out.abs().max() <= 1.0
+    assert out.std() > 0.05  # not collapsed
+    again = g.inference(mel)
+    assert torch.equal(out, again), "run-to-run determinism"
+    for i in (0, 17, 31):
+        single = g.inference(mel[i : i + 1])
+        assert torch.equal(single[0], out[i]), f"batch invariance, item {i}"
+    ref = hifigan_ref.hifigan_forward(sd, mel[17:18].cpu(), pad=5, dtype=torch.float64, **V1)
+    assert_close_fp32(out[17:18].cpu(), ref, "B=32 item 17 vs fp64 oracle")

@@ -1,0 +1,260 @@
+// extern "C" entry points of libtts_mi355x.so (declared in include/tts_mi355x.h).
+// Every call converts library exceptions into a status code + thread-local message.
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "glow.hpp"
+#include "hifigan.hpp"
+#include "tts_mi355x.h"
+
+namespace {
+thread_local std::string g_last_error;
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    g_last_error.clear();
+    f();
+    return TTS_OK;
+  } catch (const tts::Error& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return TTS_ERR_OOM;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TTS_ERR_INVALID;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return TTS_ERR_INVALID;
+  }
+}
+
+// RAII device buffer for the single-op entry points.
+struct TmpDev {
+  float* p = nullptr;
+  explicit TmpDev(const float* host, size_t n) {
+    if (n == 0) return;
+    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) throw tts::Error(4, "hipMalloc failed");
+    TTS_HIP_CHECK(hipMemcpy(p, host, n * sizeof(float), hipMemcpyHostToDevice));
+  }
+  ~TmpDev() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+extern "C" {
+
+const char* tts_last_error(void) { return g_last_error.c_str(); }
+int tts_abi_version(void) { return 100; }
+const char* tts_build_target(void) { return "gfx950"; }
+
+// ----------------------------------------------------------------------------- HiFiGAN
+int tts_hifigan_num_weights(const TtsHifiganCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::hifigan_validate(*cfg);
+    n = (int)tts::hifigan_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_hifigan_weight_numel(const TtsHifiganCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::hifigan_validate(*cfg);
+    auto s = tts::hifigan_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_hifigan_create(const TtsHifiganCfg* cfg, const float* const* host_weights, int device,
+                       void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::Hifigan(*cfg, host_weights, device);
+  });
+}
+
+int tts_hifigan_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::Hifigan*>(handle); });
+}
+
+int64_t tts_hifigan_output_length(const void* handle, int T, int pad) {
+  if (!handle) return -1;
+  return static_cast<const tts::Hifigan*>(handle)->out_len(T, pad);
+}
+
+int64_t tts_hifigan_workspace_bytes(const void* handle, int B, int T, int pad) {
+  if (!handle) return -1;
+  return static_cast<const tts::Hifigan*>(handle)->workspace_bytes(B, T, pad);
+}
+
+int tts_hifigan_reserve(void* handle, int B, int T, int pad) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    TTS_REQUIRE(B >= 1 && T >= 1 && pad >= 0, 1, "bad shape");
+    static_cast<tts::Hifigan*>(handle)->reserve(B, T, pad);
+  });
+}
+
+int tts_hifigan_forward(void* handle, const float* d_mel, int B, int C, int T, int pad,
+                        const float* d_g, float* d_wav, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::Hifigan*>(handle)->forward(d_mel, B, C, T, pad, d_g, d_wav,
+                                                static_cast<hipStream_t>(hip_stream), nullptr);
+  });
+}
+
+int tts_hifigan_forward_profiled(void* handle, const float* d_mel, int B, int C, int T, int pad,
+                                 const float* d_g, float* d_wav, void* hip_stream,
+                                 TtsLaunchRecord* records, int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::Hifigan*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->forward(d_mel, B, C, T, pad, d_g, d_wav, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    *n_records = (int)prof.recs.size();
+    for (int i = 0; i < (int)prof.recs.size() && i < max_records && records; ++i) {
+      auto& r = prof.recs[i];
+      std::memset(records[i].name, 0, sizeof(records[i].name));
+      std::strncpy(records[i].name, r.name.c_str(), sizeof(records[i].name) - 1);
+      records[i].flops = r.flops;
+      records[i].bytes = r.bytes;
+      float ms = 0.f;
+      TTS_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+      records[i].ms = ms;
+    }
+  });
+}
+
+// ----------------------------------------------------------------------------- Glow decoder
+int tts_glow_decoder_num_weights(const TtsGlowDecoderCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::glow_validate(*cfg);
+    n = (int)tts::glow_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_glow_decoder_weight_numel(const TtsGlowDecoderCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::glow_validate(*cfg);
+    auto s = tts::glow_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_glow_decoder_create(const TtsGlowDecoderCfg* cfg, const float* const* host_weights,
+                            int device, void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::GlowDecoder(*cfg, host_weights, device);
+  });
+}
+
+int tts_glow_decoder_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::GlowDecoder*>(handle); });
+}
+
+int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, int B, int C,
+                             int T, int reverse, float* d_y, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    static_cast<tts::GlowDecoder*>(handle)->reverse(d_x, d_mask, B, C, T, d_y,
+                                                    static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+// ----------------------------------------------------------------------------- single ops
+int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
+                  const float* d_res, float* d_y, float* d_z, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d && d_x && h_w && h_b, 1, "NULL argument");
+    TTS_REQUIRE(d->B >= 1 && d->Cin >= 1 && d->Cout >= 1 && d->Tin >= 1 && d->K >= 1 && d->dil >= 1, 1,
+                "bad conv1d shape");
+    TTS_REQUIRE((d->K % 2) == 1, 3, "conv1d: only odd kernel sizes ('same' padding)");
+    TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
+    TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
+    const int tile = tts::conv1d_tile_for(d->Cout, d->K);
+    const tts::ConvTile t = tts::conv1d_tile(tile);
+    std::vector<float> packed(tts::packed_conv1d_numel(d->Cout, d->Cin, d->K, t));
+    tts::pack_conv1d(h_w, d->Cout, d->Cin, d->K, t, packed.data());
+    std::vector<float> bias((size_t)tts::ceil_div(d->Cout, t.BM) * t.BM, 0.f);
+    std::memcpy(bias.data(), h_b, sizeof(float) * d->Cout);
+    TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
+    tts::Conv1dArgs a{};
+    a.x = d_x; a.w = w.p; a.bias = b.p; a.res = d_res; a.y = d_y; a.z = d_z; a.cvec = nullptr;
+    a.Cin = d->Cin; a.Cout = d->Cout; a.Tin = d->Tin; a.Tout = d->Tin + 2 * d->rep_pad;
+    a.dil = d->dil; a.pad = d->dil * (d->K - 1) / 2; a.rep_pad = d->rep_pad;
+    a.n_chunks = tts::ceil_div(d->Cin, t.CK);
+    a.in_slope = d->in_slope; a.out_slope = d->out_slope; a.zmode = d->zmode; a.zdiv = d->zdiv;
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::launch_conv1d(a, d->B, d->K, tile, s);
+    TTS_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
+                            const float* h_b, int Cout, int K, int stride, float in_slope,
+                            float* d_y, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_x && h_w && h_b && d_y, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && Cin >= 1 && Cout >= 1 && Tin >= 1, 1, "bad conv_transpose1d shape");
+    TTS_REQUIRE(K == 2 * stride, 3, "conv_transpose1d: requires kernel_size == 2*stride");
+    const int tile = tts::convT_tile_for(Cout, stride);
+    const tts::ConvTile t = tts::convT_tile(tile, stride);
+    std::vector<float> packed(tts::packed_convT_numel(Cin, Cout, stride, t));
+    tts::pack_convT(h_w, Cin, Cout, stride, t, packed.data());
+    std::vector<float> bias((size_t)tts::ceil_div(Cout, t.BM) * t.BM, 0.f);
+    std::memcpy(bias.data(), h_b, sizeof(float) * Cout);
+    TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
+    tts::ConvTArgs a{};
+    a.x = d_x; a.w = w.p; a.bias = b.p; a.y = d_y;
+    a.Cin = Cin; a.Cout = Cout; a.Tin = Tin; a.n_chunks = tts::ceil_div(Cin, t.CK); a.in_slope = in_slope;
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::launch_convT(a, B, stride, tile, s);
+    TTS_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+int tts_op_conv_post(const float* d_z, int B, int Cin, int T, const float* h_w, const float* h_b,
+                     float in_slope, float* d_y, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_z && h_w && d_y, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && Cin >= 1 && T >= 1, 1, "bad conv_post shape");
+    TmpDev w(h_w, (size_t)Cin * 7);
+    tts::PostArgs a{};
+    a.z = d_z; a.w = w.p; a.bias = h_b ? h_b[0] : 0.f; a.y = d_y; a.Cin = Cin; a.T = T; a.in_slope = in_slope;
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::launch_conv_post(a, B, s);
+    TTS_HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+}  // extern "C"

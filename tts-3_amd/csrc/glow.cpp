@@ -1,0 +1,199 @@
+// Glow-TTS decoder flow, reverse direction, on the MFMA conv kernel + fused elementwise tails.
+// Reference: TTS/tts/layers/glow_tts/decoder.py:113-137, glow.py:102-137 and :201-230,
+// wavenet.py:94-115, normalization.py:88-103.
+#include "glow.hpp"
+
+#include <cstring>
+
+namespace tts {
+
+std::vector<int64_t> glow_weight_shapes(const TtsGlowDecoderCfg& c) {
+  std::vector<int64_t> n;
+  const int C2 = c.in_channels * c.num_squeeze;
+  const int H = c.hidden_channels;
+  const int S = c.num_splits;
+  for (int f = 0; f < c.num_flow_blocks; ++f) {
+    n.push_back(C2);                      // actnorm.logs
+    n.push_back(C2);                      // actnorm.bias
+    n.push_back((int64_t)S * S);          // invconv.weight_inv
+    n.push_back((int64_t)H * (C2 / 2));   // start.weight
+    n.push_back(H);                       // start.bias
+    for (int l = 0; l < c.num_coupling_layers; ++l) {
+      n.push_back((int64_t)2 * H * H * c.kernel_size);
+      n.push_back(2 * H);
+      const int rsc = (l < c.num_coupling_layers - 1) ? 2 * H : H;
+      n.push_back((int64_t)rsc * H);
+      n.push_back(rsc);
+    }
+    n.push_back((int64_t)C2 * H);  // end.weight
+    n.push_back(C2);               // end.bias
+  }
+  return n;
+}
+
+void glow_validate(const TtsGlowDecoderCfg& c) {
+  TTS_REQUIRE(c.in_channels >= 1 && c.hidden_channels >= 2 && c.num_flow_blocks >= 1 &&
+                  c.num_coupling_layers >= 1,
+              1, "bad Glow decoder configuration");
+  TTS_REQUIRE(c.num_squeeze >= 1, 1, "num_squeeze must be >= 1");
+  TTS_REQUIRE(c.num_splits == 2 || c.num_splits == 4 || c.num_splits == 8, 3, "num_splits must be 2, 4 or 8");
+  TTS_REQUIRE((c.in_channels * c.num_squeeze) % c.num_splits == 0, 1,
+              "channels*num_squeeze must be divisible by num_splits (glow.py:109)");
+  TTS_REQUIRE((c.in_channels * c.num_squeeze) % 2 == 0, 1, "coupling needs an even channel count");
+  TTS_REQUIRE(c.kernel_size % 2 == 1, 1, "kernel_size must be odd (wavenet.py:49)");
+  TTS_REQUIRE(c.kernel_size == 1 || c.kernel_size == 3 || c.kernel_size == 5 || c.kernel_size == 7 ||
+                  c.kernel_size == 11,
+              3, "kernel_size must be 1, 3, 5, 7 or 11");
+  int d = 1;
+  for (int l = 0; l < c.num_coupling_layers; ++l) {
+    TTS_REQUIRE((c.kernel_size - 1) * d <= 96, 3, "(kernel_size-1)*dilation above 96 is not implemented");
+    d *= c.dilation_rate;
+  }
+  TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned Glow decoder (c_in_channels > 0) not implemented");
+}
+
+GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, int device)
+    : cfg_(cfg), device_(device) {
+  glow_validate(cfg_);
+  DeviceGuard g(device_);
+  const auto shapes = glow_weight_shapes(cfg_);
+  for (size_t i = 0; i < shapes.size(); ++i)
+    TTS_REQUIRE(hw[i] != nullptr, 1, "weight pointer " + std::to_string(i) + " is NULL");
+  const int C2 = cfg_.in_channels * cfg_.num_squeeze;
+  const int H = cfg_.hidden_channels;
+  const int S = cfg_.num_splits;
+  const int L = cfg_.num_coupling_layers;
+
+  std::vector<float> host;
+  auto align = [](size_t n) { return (n + 63) & ~size_t(63); };
+  struct Pending { size_t off; float** dst; };
+  std::vector<std::pair<size_t, float**>> fix;  // (offset, pointer to patch)
+  auto put = [&](const float* src, size_t n, float** dst) {
+    const size_t off = host.size();
+    host.resize(off + align(n), 0.f);
+    std::memcpy(host.data() + off, src, n * sizeof(float));
+    fix.push_back({off, dst});
+  };
+  auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
+    cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
+    cv.tile = conv1d_tile_for(Cout, K);
+    const ConvTile t = conv1d_tile(cv.tile);
+    cv.n_chunks = ceil_div(Cin, t.CK);
+    const size_t n = packed_conv1d_numel(Cout, Cin, K, t);
+    const size_t off = host.size();
+    host.resize(off + align(n), 0.f);
+    pack_conv1d(w, Cout, Cin, K, t, host.data() + off);
+    fix.push_back({off, &cv.w});
+    const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
+    const size_t offb = host.size();
+    host.resize(offb + align(nb), 0.f);
+    std::memcpy(host.data() + offb, b, Cout * sizeof(float));
+    fix.push_back({offb, &cv.b});
+  };
+
+  flows_.resize(cfg_.num_flow_blocks);
+  size_t wi = 0;
+  for (int f = 0; f < cfg_.num_flow_blocks; ++f) {
+    Flow& F = flows_[f];
+    put(hw[wi], C2, &F.logs); put(hw[wi + 1], C2, &F.bias); put(hw[wi + 2], (size_t)S * S, &F.winv);
+    wi += 3;
+    put_conv(F.start, hw[wi], hw[wi + 1], C2 / 2, H, 1, 1); wi += 2;
+    F.in_layers.resize(L); F.res_skip.resize(L);
+    int d = 1;
+    for (int l = 0; l < L; ++l) {
+      put_conv(F.in_layers[l], hw[wi], hw[wi + 1], H, 2 * H, cfg_.kernel_size, d); wi += 2;
+      const int rsc = (l < L - 1) ? 2 * H : H;
+      put_conv(F.res_skip[l], hw[wi], hw[wi + 1], H, rsc, 1, 1); wi += 2;
+      d *= cfg_.dilation_rate;
+    }
+    put_conv(F.end, hw[wi], hw[wi + 1], H, C2, 1, 1); wi += 2;
+  }
+  if (hipMalloc(&arena_, host.size() * sizeof(float)) != hipSuccess) throw Error(4, "hipMalloc(weights) failed");
+  TTS_HIP_CHECK(hipMemcpy(arena_, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+  for (auto& p : fix) *p.second = arena_ + p.first;
+}
+
+GlowDecoder::~GlowDecoder() {
+  DeviceGuard g(device_);
+  if (arena_) (void)hipFree(arena_);
+  if (ws_) (void)hipFree(ws_);
+}
+
+void GlowDecoder::reserve(int B, int Th) {
+  const int C2 = cfg_.in_channels * cfg_.num_squeeze;
+  const int H = cfg_.hidden_channels;
+  const size_t plane = (size_t)B * Th;
+  // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1
+  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 8 * sizeof(float);
+  if (need <= ws_bytes_) return;
+  if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
+  if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
+  ws_bytes_ = need;
+}
+
+void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s) {
+  TTS_REQUIRE(x && mask && y, 1, "NULL input/output pointer");
+  TTS_REQUIRE(B >= 1, 1, "batch must be >= 1");
+  TTS_REQUIRE(C == cfg_.in_channels, 1, "channel count does not match the decoder");
+  const int nsq = cfg_.num_squeeze;
+  const int Th = T / nsq;
+  TTS_REQUIRE(Th >= 1, 1, "T too short for num_squeeze");
+  DeviceGuard g(device_);
+  reserve(B, Th);
+  const int C2 = C * nsq;
+  const int H = cfg_.hidden_channels;
+  const int L = cfg_.num_coupling_layers;
+  const size_t plane = (size_t)B * Th;
+  auto al = [](size_t n) { return (n + 63) & ~size_t(63); };
+  float* p = ws_;
+  float* xs = p; p += al(plane * C2);
+  float* hb = p; p += al(plane * H);
+  float* xin = p; p += al(plane * 2 * H);
+  float* acts = p; p += al(plane * H);
+  float* rs = p; p += al(plane * 2 * H);
+  float* skip = p; p += al(plane * H);
+  float* out = p; p += al(plane * C2);
+  float* msq = p;
+
+  // squeeze (decoder.py:128, :8-28); without squeeze the mask is used as is
+  if (nsq > 1) {
+    launch_glow_squeeze(x, mask, xs, msq, B, C, T, nsq, s);
+  } else {
+    TTS_HIP_CHECK(hipMemcpyAsync(xs, x, plane * C2 * sizeof(float), hipMemcpyDeviceToDevice, s));
+    TTS_HIP_CHECK(hipMemcpyAsync(msq, mask, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
+  }
+
+  auto conv = [&](const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m) {
+    Conv1dArgs a{};
+    a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride;
+    a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th;
+    a.dil = cv.dil; a.pad = cv.dil * (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;
+    a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = 0; a.zdiv = 1.f;
+    launch_conv1d(a, B, cv.K, cv.tile, s);
+  };
+
+  // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1
+  for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
+    const Flow& F = flows_[f];
+    // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
+    conv(F.start, xs, (int64_t)C2 * Th, hb, msq);
+    for (int l = 0; l < L; ++l) {
+      conv(F.in_layers[l], hb, 0, xin, nullptr);                 // wavenet.py:101
+      launch_glow_gate(xin, acts, B, H, Th, s);                  // :108
+      conv(F.res_skip[l], acts, 0, rs, nullptr);                 // :109
+      launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s);  // :110-115
+    }
+    conv(F.end, skip, 0, out, nullptr);                          // glow.py:214
+    GlowTailArgs ta{};
+    ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
+    ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
+    launch_glow_tail(ta, B, s);
+  }
+  if (nsq > 1) {
+    launch_glow_unsqueeze(xs, msq, y, B, C, Th, nsq, s);
+  } else {
+    TTS_HIP_CHECK(hipMemcpyAsync(y, xs, plane * C2 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  }
+}
+
+}  // namespace tts

@@ -1,0 +1,68 @@
+// Glow-TTS decoder flow executor, reverse direction
+// (TTS/tts/layers/glow_tts/decoder.py:113-137 with reverse=True).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "hifigan.hpp"
+#include "tts_mi355x.h"
+
+namespace tts {
+
+std::vector<int64_t> glow_weight_shapes(const TtsGlowDecoderCfg& c);
+void glow_validate(const TtsGlowDecoderCfg& c);
+
+// Elementwise kernels of the flow (kernels_glow.hip).
+struct GlowTailArgs {
+  float* x;            // [B][C2][Th], updated in place
+  const float* out;    // [B][C2][Th] = end(WN(...)): rows [0,C2/2) = t, [C2/2,C2) = s
+  const float* mask;   // [B][Th]
+  const float* winv;   // [S][S] device
+  const float* logs;   // [C2]
+  const float* bias;   // [C2]
+  int C2, Th, S;
+  int sigmoid_scale;
+};
+void launch_glow_squeeze(const float* x, const float* mask, float* xs, float* msq, int B, int C, int T,
+                         int nsq, hipStream_t s);
+void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, int C, int Th, int nsq,
+                           hipStream_t s);
+void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s);
+void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,
+                           int Th, int first, int last, hipStream_t s);
+void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s);
+
+class GlowDecoder {
+ public:
+  GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* host_weights, int device);
+  ~GlowDecoder();
+  GlowDecoder(const GlowDecoder&) = delete;
+  GlowDecoder& operator=(const GlowDecoder&) = delete;
+  void reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s);
+
+ private:
+  struct Conv {
+    int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+  };
+  struct Flow {
+    float* logs = nullptr;
+    float* bias = nullptr;
+    float* winv = nullptr;
+    Conv start, end;
+    std::vector<Conv> in_layers, res_skip;
+  };
+  void reserve(int B, int Th);
+
+  TtsGlowDecoderCfg cfg_;
+  int device_;
+  std::vector<Flow> flows_;
+  float* arena_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+}  // namespace tts

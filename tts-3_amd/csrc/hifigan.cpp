@@ -1,0 +1,335 @@
+// HiFiGAN generator executor: builds the launch plan of HifiganGenerator.forward
+// (TTS/vocoder/models/hifigan_generator.py:236-265) from the constructor arguments,
+// owns the packed weights and the activation workspace in HBM, and enqueues the kernels
+// on the caller's stream.
+#include "hifigan.hpp"
+
+#include <cstring>
+#include <vector>
+
+namespace tts {
+
+namespace {
+bool valid_conv_k(int k) { return k == 1 || k == 3 || k == 5 || k == 7 || k == 11; }
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Weight inventory (order documented in tts_mi355x.h)
+// ---------------------------------------------------------------------------------------
+std::vector<int64_t> hifigan_weight_shapes(const TtsHifiganCfg& c) {
+  std::vector<int64_t> n;
+  const int C0 = c.upsample_initial_channel;
+  n.push_back((int64_t)C0 * c.in_channels * 7);
+  n.push_back(C0);
+  for (int i = 0; i < c.num_upsamples; ++i) {
+    const int ci = C0 >> i, co = C0 >> (i + 1);
+    n.push_back((int64_t)ci * co * c.upsample_kernel_sizes[i]);
+    n.push_back(co);
+  }
+  for (int i = 0; i < c.num_upsamples; ++i) {
+    const int ch = C0 >> (i + 1);
+    for (int j = 0; j < c.num_kernels; ++j) {
+      const int k = c.resblock_kernel_sizes[j];
+      const int nconv = (c.resblock_type == 1) ? 6 : 2;
+      for (int m = 0; m < nconv; ++m) {
+        n.push_back((int64_t)ch * ch * k);
+        n.push_back(ch);
+      }
+    }
+  }
+  const int cl = C0 >> c.num_upsamples;
+  n.push_back((int64_t)c.out_channels * cl * 7);
+  if (c.conv_post_bias) n.push_back(c.out_channels);
+  if (c.cond_channels > 0) {
+    n.push_back((int64_t)C0 * c.cond_channels);
+    n.push_back(C0);
+  }
+  return n;
+}
+
+void hifigan_validate(const TtsHifiganCfg& c) {
+  TTS_REQUIRE(c.in_channels >= 1, 1, "in_channels must be >= 1");
+  TTS_REQUIRE(c.out_channels == 1, 3, "only out_channels == 1 is implemented");
+  TTS_REQUIRE(c.resblock_type == 1 || c.resblock_type == 2, 1, "resblock_type must be '1' or '2'");
+  TTS_REQUIRE(c.num_kernels >= 1 && c.num_kernels <= TTS_MAX_KERNELS, 1, "bad num_kernels");
+  TTS_REQUIRE(c.num_upsamples >= 1 && c.num_upsamples <= TTS_MAX_UPSAMPLES, 1, "bad num_upsamples");
+  const int need_d = c.resblock_type == 1 ? 3 : 2;
+  TTS_REQUIRE(c.num_dilations >= need_d && c.num_dilations <= TTS_MAX_DILATIONS, 1,
+              "resblock_dilation_sizes too short for the resblock type");
+  for (int j = 0; j < c.num_kernels; ++j) {
+    TTS_REQUIRE(valid_conv_k(c.resblock_kernel_sizes[j]), 3,
+                "resblock kernel size " + std::to_string(c.resblock_kernel_sizes[j]) +
+                    " not implemented (1,3,5,7,11)");
+    for (int m = 0; m < need_d; ++m) {
+      const int d = c.resblock_dilation_sizes[j][m];
+      TTS_REQUIRE(d >= 1 && (c.resblock_kernel_sizes[j] - 1) * d <= 96, 3,
+                  "resblock (kernel_size-1)*dilation must be <= 96");
+    }
+  }
+  int C = c.upsample_initial_channel;
+  for (int i = 0; i < c.num_upsamples; ++i) {
+    const int u = c.upsample_factors[i];
+    TTS_REQUIRE(u == 2 || u == 4 || u == 8, 3, "upsample factor must be 2, 4 or 8");
+    TTS_REQUIRE(c.upsample_kernel_sizes[i] == 2 * u, 3,
+                "upsample kernel size must equal 2*factor (polyphase kernel)");
+    C >>= 1;
+    TTS_REQUIRE(C >= 1, 1, "upsample_initial_channel too small for the number of upsamples");
+  }
+  TTS_REQUIRE(c.inference_padding >= 0, 1, "inference_padding must be >= 0");
+  TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
+}
+
+// ---------------------------------------------------------------------------------------
+Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
+    : cfg_(cfg), device_(device) {
+  hifigan_validate(cfg_);
+  DeviceGuard g(device_);
+  const auto shapes = hifigan_weight_shapes(cfg_);
+  for (size_t i = 0; i < shapes.size(); ++i)
+    TTS_REQUIRE(hw[i] != nullptr, 1, "weight pointer " + std::to_string(i) + " is NULL");
+
+  // 1) describe layers, 2) size the arena, 3) pack on host, 4) one upload.
+  const int C0 = cfg_.upsample_initial_channel;
+  size_t wi = 0;
+  std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
+  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam) {
+    ConvLayer L;
+    L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
+    L.tile = conv1d_tile_for(Cout, K);
+    const ConvTile t = conv1d_tile(L.tile);
+    L.n_chunks = ceil_div(Cin, t.CK);
+    L.w_numel = packed_conv1d_numel(Cout, Cin, K, t);
+    L.b_numel = (int64_t)ceil_div(Cout, t.BM) * t.BM;
+    L.name = std::string(fam) + "_k" + std::to_string(K) + "_c" + std::to_string(Cout);
+    return L;
+  };
+
+  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre");
+  src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    ConvTLayer L;
+    L.Cin = C0 >> i; L.Cout = C0 >> (i + 1); L.U = cfg_.upsample_factors[i];
+    L.tile = convT_tile_for(L.Cout, L.U);
+    const ConvTile t = convT_tile(L.tile, L.U);
+    L.n_chunks = ceil_div(L.Cin, t.CK);
+    L.w_numel = packed_convT_numel(L.Cin, L.Cout, L.U, t);
+    L.b_numel = (int64_t)ceil_div(L.Cout, t.BM) * t.BM;
+    L.name = "ups_u" + std::to_string(L.U) + "_c" + std::to_string(L.Cout);
+    ups_.push_back(L);
+  }
+  std::vector<std::pair<const float*, const float*>> usrc;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) { usrc.push_back({hw[wi], hw[wi + 1]}); wi += 2; }
+
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    const int ch = C0 >> (i + 1);
+    for (int j = 0; j < cfg_.num_kernels; ++j) {
+      const int k = cfg_.resblock_kernel_sizes[j];
+      ResBlock rb;
+      if (cfg_.resblock_type == 1) {
+        // state_dict order: convs1.0..2 then convs2.0..2
+        const float* w1[3]; const float* b1[3]; const float* w2[3]; const float* b2[3];
+        for (int m = 0; m < 3; ++m) { w1[m] = hw[wi]; b1[m] = hw[wi + 1]; wi += 2; }
+        for (int m = 0; m < 3; ++m) { w2[m] = hw[wi]; b2[m] = hw[wi + 1]; wi += 2; }
+        for (int m = 0; m < 3; ++m) {
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv"));
+          src.push_back({w1[m], b1[m]});
+          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv"));
+          src.push_back({w2[m], b2[m]});
+        }
+      } else {
+        for (int m = 0; m < 2; ++m) {
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv"));
+          src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
+        }
+      }
+      res_.push_back(rb);
+    }
+  }
+  post_w_ = hw[wi]; wi += 1;
+  post_bias_ = cfg_.conv_post_bias ? hw[wi][0] : 0.f;
+  if (cfg_.conv_post_bias) wi += 1;
+  const float* cond_w = nullptr; const float* cond_b = nullptr;
+  if (cfg_.cond_channels > 0) { cond_w = hw[wi]; cond_b = hw[wi + 1]; wi += 2; }
+
+  // arena layout
+  std::vector<ConvLayer*> convs;
+  convs.push_back(&pre_);
+  for (auto& rb : res_) for (auto& c : rb.convs) convs.push_back(&c);
+  int64_t total = 0;
+  auto align = [](int64_t n) { return (n + 63) & ~int64_t(63); };
+  for (auto* c : convs) total += align(c->w_numel) + align(c->b_numel);
+  for (auto& u : ups_) total += align(u.w_numel) + align(u.b_numel);
+  const int Cl = C0 >> cfg_.num_upsamples;
+  total += align((int64_t)Cl * 7);
+  if (cfg_.cond_channels > 0) total += align((int64_t)C0 * cfg_.cond_channels) + align(C0);
+
+  std::vector<float> host(total, 0.f);
+  int64_t off = 0;
+  std::vector<int64_t> offs;
+  // conv1d layers: src[] is in the same order as convs[] (pre, then resblock convs)
+  // resblock convs were pushed in execution order (c1_0, c2_0, c1_1, ...), matching src.
+  {
+    // src[0] is conv_pre; src[1..] resblocks
+    size_t si = 0;
+    for (auto* c : convs) {
+      const ConvTile t = conv1d_tile(c->tile);
+      pack_conv1d(src[si].first, c->Cout, c->Cin, c->K, t, host.data() + off);
+      offs.push_back(off); off += align(c->w_numel);
+      std::memcpy(host.data() + off, src[si].second, sizeof(float) * c->Cout);
+      offs.push_back(off); off += align(c->b_numel);
+      ++si;
+    }
+  }
+  for (size_t i = 0; i < ups_.size(); ++i) {
+    auto& u = ups_[i];
+    const ConvTile t = convT_tile(u.tile, u.U);
+    pack_convT(usrc[i].first, u.Cin, u.Cout, u.U, t, host.data() + off);
+    offs.push_back(off); off += align(u.w_numel);
+    std::memcpy(host.data() + off, usrc[i].second, sizeof(float) * u.Cout);
+    offs.push_back(off); off += align(u.b_numel);
+  }
+  std::memcpy(host.data() + off, post_w_, sizeof(float) * Cl * 7);
+  const int64_t post_off = off; off += align((int64_t)Cl * 7);
+  int64_t cond_w_off = -1, cond_b_off = -1;
+  if (cfg_.cond_channels > 0) {
+    std::memcpy(host.data() + off, cond_w, sizeof(float) * C0 * cfg_.cond_channels);
+    cond_w_off = off; off += align((int64_t)C0 * cfg_.cond_channels);
+    std::memcpy(host.data() + off, cond_b, sizeof(float) * C0);
+    cond_b_off = off; off += align(C0);
+  }
+
+  weights_bytes_ = (size_t)total * sizeof(float);
+  if (hipMalloc(&arena_, weights_bytes_) != hipSuccess) throw Error(4, "hipMalloc(weights) failed");
+  TTS_HIP_CHECK(hipMemcpy(arena_, host.data(), weights_bytes_, hipMemcpyHostToDevice));
+  size_t oi = 0;
+  for (auto* c : convs) { c->w = arena_ + offs[oi++]; c->b = arena_ + offs[oi++]; }
+  for (auto& u : ups_) { u.w = arena_ + offs[oi++]; u.b = arena_ + offs[oi++]; }
+  post_wd_ = arena_ + post_off;
+  if (cfg_.cond_channels > 0) { cond_wd_ = arena_ + cond_w_off; cond_bd_ = arena_ + cond_b_off; }
+  hop_ = 1;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) hop_ *= cfg_.upsample_factors[i];
+}
+
+Hifigan::~Hifigan() {
+  DeviceGuard g(device_);
+  if (arena_) (void)hipFree(arena_);
+  if (ws_) (void)hipFree(ws_);
+}
+
+int64_t Hifigan::out_len(int T, int pad) const { return (int64_t)hop_ * (T + 2 * pad); }
+
+int64_t Hifigan::plane_floats(int B, int T, int pad) const {
+  // largest C_i * len_i over the stages (conv_pre output included)
+  const int64_t L = T + 2 * pad;
+  int64_t best = (int64_t)cfg_.upsample_initial_channel * L;
+  int64_t len = L;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    len *= cfg_.upsample_factors[i];
+    const int64_t c = (int64_t)(cfg_.upsample_initial_channel >> (i + 1)) * len;
+    if (c > best) best = c;
+  }
+  return ((best * B + 63) / 64) * 64;
+}
+
+int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
+  const int64_t cond = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
+  return (4 * plane_floats(B, T, pad) + cond) * (int64_t)sizeof(float);
+}
+
+void Hifigan::reserve(int B, int T, int pad) {
+  const int64_t need = workspace_bytes(B, T, pad);
+  if ((size_t)need <= ws_bytes_) return;
+  DeviceGuard g(device_);
+  if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
+  if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
+  ws_bytes_ = need;
+}
+
+void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const float* gvec, float* wav,
+                      hipStream_t s, Profiler* prof) {
+  TTS_REQUIRE(mel && wav, 1, "NULL input/output pointer");
+  TTS_REQUIRE(B >= 1, 1, "batch must be >= 1");
+  TTS_REQUIRE(C == cfg_.in_channels, 1,
+              "mel has " + std::to_string(C) + " channels, generator expects " + std::to_string(cfg_.in_channels));
+  TTS_REQUIRE(T >= 1, 1, "T must be >= 1");
+  TTS_REQUIRE(pad >= 0, 1, "pad must be >= 0");
+  TTS_REQUIRE(cfg_.cond_channels == 0 || gvec != nullptr, 1, "cond_channels > 0 requires g");
+  DeviceGuard g(device_);
+  reserve(B, T, pad);
+
+  const int64_t plane = plane_floats(B, T, pad);
+  float* bufZ = ws_;              // conv_pre output, then the MRF sum of each stage
+  float* bufO = ws_ + plane;      // upsampled stage input o
+  float* bufX = ws_ + 2 * plane;  // resblock running residual x
+  float* bufT = ws_ + 3 * plane;  // convs1 output (already leaky-relu'd)
+  float* cvec = cfg_.cond_channels > 0 ? ws_ + 4 * plane : nullptr;
+
+  const int L = T + 2 * pad;
+  const int C0 = cfg_.upsample_initial_channel;
+  if (cvec) {
+    run(prof, s, "cond_layer", 2.0 * B * C0 * cfg_.cond_channels, 4.0 * (B * cfg_.cond_channels + C0 * cfg_.cond_channels + B * C0),
+        [&] { launch_cond_vec(gvec, cond_wd_, cond_bd_, cvec, B, cfg_.cond_channels, C0, s); });
+  }
+
+  auto conv = [&](const ConvLayer& Ld, const float* x, int Tin, int Tout, int rep, float in_slope,
+                  float out_slope, const float* res, float* y, int zmode, const float* cv) {
+    Conv1dArgs a{};
+    a.x = x; a.w = Ld.w; a.bias = Ld.b; a.res = res; a.y = y; a.z = bufZ; a.cvec = cv;
+    a.Cin = Ld.Cin; a.Cout = Ld.Cout; a.Tin = Tin; a.Tout = Tout;
+    a.dil = Ld.dil; a.pad = Ld.pad; a.rep_pad = rep; a.n_chunks = Ld.n_chunks;
+    a.in_slope = in_slope; a.out_slope = out_slope; a.zmode = zmode; a.zdiv = (float)cfg_.num_kernels;
+    const double flops = 2.0 * B * Ld.Cout * (double)Ld.Cin * Ld.K * Tout;
+    double bytes = 4.0 * ((double)B * Ld.Cin * Tin + (double)Ld.Cout * Ld.Cin * Ld.K + (double)B * Ld.Cout * Tout);
+    if (res) bytes += 4.0 * B * Ld.Cout * (double)Tout;
+    if (zmode >= 2) bytes += 4.0 * B * Ld.Cout * (double)Tout;
+    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv1d(a, B, Ld.K, Ld.tile, s); });
+  };
+
+  // conv_pre on the replicate-padded mel (hifigan_generator.py:281, :249) [+ cond_layer(g), :250-251]
+  conv(pre_, mel, T, L, pad, 1.f, 1.f, nullptr, bufZ, 0, cvec);
+
+  int len = L;
+  const float* cur = bufZ;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    const ConvTLayer& U = ups_[i];
+    ConvTArgs ta{};
+    ta.x = cur; ta.w = U.w; ta.bias = U.b; ta.y = bufO;
+    ta.Cin = U.Cin; ta.Cout = U.Cout; ta.Tin = len; ta.n_chunks = U.n_chunks; ta.in_slope = 0.1f;
+    const int lout = len * U.U;
+    run(prof, s, U.name.c_str(), 2.0 * B * U.Cout * (double)U.Cin * 2 * lout,
+        4.0 * ((double)B * U.Cin * len + (double)U.Cin * U.Cout * 2 * U.U + (double)B * U.Cout * lout),
+        [&] { launch_convT(ta, B, U.U, U.tile, s); });
+    len = lout;
+    // MRF: z = sum_j resblock_j(o); o = z / num_kernels (:255-261)
+    for (int j = 0; j < cfg_.num_kernels; ++j) {
+      const ResBlock& rb = res_[i * cfg_.num_kernels + j];
+      const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
+      if (cfg_.resblock_type == 1) {
+        for (int m = 0; m < 3; ++m) {
+          const float* xin = (m == 0) ? bufO : bufX;
+          // xt = convs1[m](lrelu(x)); xt = lrelu(xt)       (ResBlock1.forward :94-96)
+          conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr);
+          // x = convs2[m](xt) + x                          (:97-98)
+          const bool last = (m == 2);
+          conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr);
+        }
+      } else {
+        for (int m = 0; m < 2; ++m) {
+          const float* xin = (m == 0) ? bufO : bufX;
+          const bool last = (m == 1);
+          // x = convs[m](lrelu(x)) + x                     (ResBlock2.forward :151-154)
+          conv(rb.convs[m], xin, len, len, 0, 0.1f, 1.f, xin, bufX, last ? zlast : 0, nullptr);
+        }
+      }
+    }
+    cur = bufZ;
+  }
+  // leaky_relu (default slope 0.01!) -> conv_post -> tanh (:262-264)
+  PostArgs pa{};
+  pa.z = bufZ; pa.w = post_wd_; pa.bias = post_bias_; pa.y = wav;
+  pa.Cin = C0 >> cfg_.num_upsamples; pa.T = len; pa.in_slope = 0.01f;
+  run(prof, s, "conv_post", 2.0 * B * len * (double)pa.Cin * 7,
+      4.0 * ((double)B * pa.Cin * len + (double)B * len), [&] { launch_conv_post(pa, B, s); });
+}
+
+}  // namespace tts

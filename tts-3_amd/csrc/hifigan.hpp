@@ -1,0 +1,112 @@
+// HiFiGAN generator executor (see hifigan.cpp) and the small host utilities it shares
+// with the Glow decoder executor.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "tts_mi355x.h"
+
+namespace tts {
+
+// Restores the caller's current HIP device on scope exit (torch keeps its own notion).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    TTS_HIP_CHECK(hipGetDevice(&prev));
+    if (prev != dev) TTS_HIP_CHECK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Per-launch hipEvent timing for *_profiled entry points.
+struct Profiler {
+  struct Rec {
+    std::string name;
+    double flops, bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  ~Profiler() {
+    for (auto& r : recs) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+  }
+};
+
+template <class F>
+void run(Profiler* p, hipStream_t s, const char* name, double flops, double bytes, F&& launch) {
+  if (!p) {
+    launch();
+    return;
+  }
+  Profiler::Rec r{name, flops, bytes, nullptr, nullptr};
+  TTS_HIP_CHECK(hipEventCreate(&r.a));
+  TTS_HIP_CHECK(hipEventCreate(&r.b));
+  TTS_HIP_CHECK(hipEventRecord(r.a, s));
+  launch();
+  TTS_HIP_CHECK(hipEventRecord(r.b, s));
+  p->recs.push_back(r);
+}
+
+std::vector<int64_t> hifigan_weight_shapes(const TtsHifiganCfg& c);
+void hifigan_validate(const TtsHifiganCfg& c);
+
+class Hifigan {
+ public:
+  Hifigan(const TtsHifiganCfg& cfg, const float* const* host_weights, int device);
+  ~Hifigan();
+  Hifigan(const Hifigan&) = delete;
+  Hifigan& operator=(const Hifigan&) = delete;
+
+  int64_t out_len(int T, int pad) const;
+  int64_t workspace_bytes(int B, int T, int pad) const;
+  void reserve(int B, int T, int pad);
+  void forward(const float* mel, int B, int C, int T, int pad, const float* g, float* wav,
+               hipStream_t s, Profiler* prof);
+  int device() const { return device_; }
+
+ private:
+  struct ConvLayer {
+    int Cin = 0, Cout = 0, K = 0, dil = 1, pad = 0, tile = 0, n_chunks = 0;
+    int64_t w_numel = 0, b_numel = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+    std::string name;
+  };
+  struct ConvTLayer {
+    int Cin = 0, Cout = 0, U = 0, tile = 0, n_chunks = 0;
+    int64_t w_numel = 0, b_numel = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+    std::string name;
+  };
+  struct ResBlock {
+    std::vector<ConvLayer> convs;  // type 1: c1_0, c2_0, c1_1, c2_1, c1_2, c2_2; type 2: c_0, c_1
+  };
+
+  int64_t plane_floats(int B, int T, int pad) const;
+
+  TtsHifiganCfg cfg_;
+  int device_;
+  int hop_ = 1;
+  ConvLayer pre_;
+  std::vector<ConvTLayer> ups_;
+  std::vector<ResBlock> res_;
+  const float* post_w_ = nullptr;  // host pointer, only valid during construction
+  float post_bias_ = 0.f;
+  float* post_wd_ = nullptr;
+  float* cond_wd_ = nullptr;
+  float* cond_bd_ = nullptr;
+  float* arena_ = nullptr;
+  size_t weights_bytes_ = 0;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+}  // namespace tts

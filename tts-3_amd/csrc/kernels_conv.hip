@@ -1,0 +1,546 @@
+// HiFiGAN hot-path kernels for gfx950 (CDNA4), fp32 in / fp32 accumulate.
+//
+// conv1d_mfma   : "same" dilated Conv1d as an implicit GEMM on v_mfma_f32_32x32x2_f32.
+//                 Reference ops: conv_pre (hifigan_generator.py:203,249), the 72 MRF convs of
+//                 ResBlock1.forward (:93-98) / ResBlock2.forward (:151-154), with the
+//                 leaky_relu before each conv fused into the LDS staging, the leaky_relu after
+//                 convs1 fused into the epilogue, the residual add (:98) and the MRF sum
+//                 z_sum += ...; o = z_sum / num_kernels (:255-261) fused into the epilogue.
+// convT_mfma    : polyphase ConvTranspose1d (ups[i], :206-218, :253-254), K == 2*stride.
+//                 All U phases of a 32-frame column block live in registers, so the epilogue
+//                 writes U contiguous output samples per lane.
+// conv_post     : leaky_relu(0.01) -> conv_post (Cout 1, k7) -> tanh (:262-264).
+//
+// Data layout: NCW fp32 in HBM, exactly the reference tensors.  Each workgroup owns a
+// [BM output channels] x [BN output samples] tile of one batch item and loops over input
+// channels in chunks of CK: the chunk's packed weights [K][CK][BM] and its input window
+// [CK][BN + (K-1)*dil] are staged in LDS once and reused by every tap and every wave.
+// Double-buffered: the next chunk is fetched to registers while the MFMAs run on the
+// current one; one barrier per chunk.
+#include "common.hpp"
+
+namespace tts {
+
+// Halo ((K-1)*dilation) the register-staged input window is sized for: the narrow variant
+// covers dilation <= 5 (HiFiGAN v1/v2, Glow WN), the wide one HiFiGAN-v3's dilation 6 / 12.
+constexpr int DMAX = 5;
+constexpr int HALO_WIDE = 96;
+
+template <int K, int BM, int BN, int TM, int TN, int CK, int HMAX>
+struct ConvCfg {
+  static constexpr int WM = BM / (32 * TM);
+  static constexpr int WN = BN / (32 * TN);
+  static constexpr int WSZ = K * CK * BM;  // floats in one weight chunk
+  static constexpr int W4 = WSZ / 4;
+  static constexpr int WPT = (W4 + 255) / 256;  // float4 per thread
+  static constexpr int XWMAX = BN + HMAX;
+  static constexpr int XSZ = CK * XWMAX;  // floats reserved for one input window
+  static constexpr int XPT = (XSZ + 255) / 256;
+  static constexpr int BUF = WSZ + XSZ;  // floats per LDS buffer (WSZ multiple of 4)
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(CK % 2 == 0, "MFMA depth is 2 channels");
+  static_assert(WSZ % 4 == 0, "");
+};
+
+template <int K, int BM, int BN, int TM, int TN, int CK, int HMAX>
+__global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
+  using C = ConvCfg<K, BM, BN, TM, TN, CK, HMAX>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / C::WN;
+  const int wn = wave % C::WN;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  const int t0 = blockIdx.x * BN;
+  const int mt = blockIdx.y;
+  const int b = blockIdx.z;
+  const int d = a.dil;
+  const int XW = BN + (K - 1) * d;
+  const int xsz = CK * XW;
+  const int Tin = a.Tin;
+  const int Tout = a.Tout;
+
+  const float* __restrict__ xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)a.Cin * Tin);
+  const f32x4* __restrict__ wg = reinterpret_cast<const f32x4*>(a.w) + (size_t)mt * a.n_chunks * C::W4;
+
+  // Chunk-invariant part of this thread's input-window gather: element e = tid + i*256
+  // of the [CK][XW] window is row r, column col -> source offset r*Tin + clamp(ts - rep).
+  int xoff[C::XPT];
+  int xrow[C::XPT];
+#pragma unroll
+  for (int i = 0; i < C::XPT; ++i) {
+    const int e = tid + i * 256;
+    const int r = e / XW;
+    const int col = e - r * XW;
+    const int ts = t0 - a.pad + col;  // position in the (replicate-)padded sequence
+    const bool ok = (e < xsz) && ts >= 0 && ts < Tout;
+    int src = ts - a.rep_pad;
+    src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
+    xoff[i] = r * Tin + src;
+    xrow[i] = ok ? r : 0x40000000;  // row index, or "never valid"
+  }
+
+  f32x4 wreg[C::WPT];
+  float xreg[C::XPT];
+
+  auto load_chunk = [&](int c) {
+    const f32x4* wc = wg + (size_t)c * C::W4;
+#pragma unroll
+    for (int i = 0; i < C::WPT; ++i) {
+      const int idx = tid + i * 256;
+      if ((C::W4 % 256) == 0 || idx < C::W4) wreg[i] = wc[idx];
+    }
+    const int rows_left = a.Cin - c * CK;  // rows of this chunk that exist
+    const float* xc = xb + (size_t)c * CK * Tin;
+#pragma unroll
+    for (int i = 0; i < C::XPT; ++i) xreg[i] = (xrow[i] < rows_left) ? xc[xoff[i]] : 0.f;
+  };
+
+  auto store_chunk = [&](int buf) {
+    f32x4* wl = reinterpret_cast<f32x4*>(smem + buf * C::BUF);
+#pragma unroll
+    for (int i = 0; i < C::WPT; ++i) {
+      const int idx = tid + i * 256;
+      if ((C::W4 % 256) == 0 || idx < C::W4) wl[idx] = wreg[i];
+    }
+    float* xl = smem + buf * C::BUF + C::WSZ;
+    const float slope = a.in_slope;
+#pragma unroll
+    for (int i = 0; i < C::XPT; ++i) {
+      const int e = tid + i * 256;
+      if (e < xsz) xl[e] = lrelu(xreg[i], slope);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
+
+  const int wcol = wm * TM * 32 + l32;          // A: output-channel lane offset
+  const int xcol = wn * TN * 32 + l32;          // B: output-time lane offset
+
+  auto compute = [&](int buf) {
+    const float* wl = smem + buf * C::BUF;
+    const float* xl = wl + C::WSZ;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int cp = 0; cp < CK / 2; ++cp) {
+        const int ci = 2 * cp + half;
+        float av[TM], bv[TN];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) av[m] = wl[(k * CK + ci) * BM + wcol + m * 32];
+#pragma unroll
+        for (int n = 0; n < TN; ++n) bv[n] = xl[ci * XW + xcol + n * 32 + k * d];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nc = a.n_chunks;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nc; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nc) load_chunk(c + 1);
+    compute(buf);
+    if (c + 1 < nc) store_chunk(buf ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue.  32x32 accumulator: lane holds column l32, rows (r&3) + 8*(r>>2) + 4*half.
+  const int Cout = a.Cout;
+  const float oslope = a.out_slope;
+  const int zmode = a.zmode;
+  const float zdiv = a.zdiv;
+  const float* __restrict__ res = a.res;
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int t = t0 + wn * TN * 32 + n * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = mt * BM + wm * TM * 32 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (co < Cout && t < Tout) {
+          const size_t idx = ((size_t)b * Cout + co) * Tout + t;
+          float v = acc[m][n][r] + a.bias[co];
+          if (a.cvec) v += a.cvec[(size_t)b * Cout + co];
+          if (a.mask) v *= a.mask[(size_t)b * Tout + t];
+          v = lrelu(v, oslope);
+          if (res) v += res[idx];
+          if (zmode == 0) {
+            a.y[idx] = v;
+          } else if (zmode == 1) {
+            a.z[idx] = v;
+          } else if (zmode == 2) {
+            a.z[idx] = a.z[idx] + v;
+          } else {
+            a.z[idx] = (a.z[idx] + v) / zdiv;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Polyphase ConvTranspose1d.  Output sample t = U*m + s - P (P = U/2, s = phase) is
+//   y[co][t] = b[co] + sum_ci W[ci][co][s] * x[ci][m] + W[ci][co][s+U] * x[ci][m-1]
+// (torch: t = i*U - P + k, k in [0, 2U)).  Frames m cover [0, Tin].
+// ---------------------------------------------------------------------------------------
+template <int U, int BM, int BN, int TM, int TN, int CK>
+struct ConvTCfg {
+  static constexpr int WM = BM / (32 * TM);
+  static constexpr int WN = BN / (32 * TN);
+  static constexpr int WSZ = 2 * U * CK * BM;
+  static constexpr int W4 = WSZ / 4;
+  static constexpr int WPT = (W4 + 255) / 256;
+  static constexpr int XW = BN + 1;
+  static constexpr int XSZ = CK * XW;
+  static constexpr int XPT = (XSZ + 255) / 256;
+  static constexpr int BUF = WSZ + ((XSZ + 3) / 4) * 4;
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(CK % 2 == 0, "");
+};
+
+template <int U, int BM, int BN, int TM, int TN, int CK>
+__global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
+  using C = ConvTCfg<U, BM, BN, TM, TN, CK>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / C::WN;
+  const int wn = wave % C::WN;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  const int m0 = blockIdx.x * BN;
+  const int mt = blockIdx.y;
+  const int b = blockIdx.z;
+  const int Tin = a.Tin;
+  const int Tout = U * Tin;
+
+  const float* __restrict__ xb = a.x + (size_t)b * a.Cin * Tin;
+  const f32x4* __restrict__ wg = reinterpret_cast<const f32x4*>(a.w) + (size_t)mt * a.n_chunks * C::W4;
+
+  int xoff[C::XPT];
+  int xrow[C::XPT];
+#pragma unroll
+  for (int i = 0; i < C::XPT; ++i) {
+    const int e = tid + i * 256;
+    const int r = e / C::XW;
+    const int col = e - r * C::XW;
+    const int ms = m0 - 1 + col;  // source frame
+    const bool ok = (e < C::XSZ) && ms >= 0 && ms < Tin;
+    xoff[i] = r * Tin + (ok ? ms : 0);
+    xrow[i] = ok ? r : 0x40000000;
+  }
+
+  f32x4 wreg[C::WPT];
+  float xreg[C::XPT];
+
+  auto load_chunk = [&](int c) {
+    const f32x4* wc = wg + (size_t)c * C::W4;
+#pragma unroll
+    for (int i = 0; i < C::WPT; ++i) {
+      const int idx = tid + i * 256;
+      if ((C::W4 % 256) == 0 || idx < C::W4) wreg[i] = wc[idx];
+    }
+    const int rows_left = a.Cin - c * CK;
+    const float* xc = xb + (size_t)c * CK * Tin;
+#pragma unroll
+    for (int i = 0; i < C::XPT; ++i) xreg[i] = (xrow[i] < rows_left) ? xc[xoff[i]] : 0.f;
+  };
+
+  auto store_chunk = [&](int buf) {
+    f32x4* wl = reinterpret_cast<f32x4*>(smem + buf * C::BUF);
+#pragma unroll
+    for (int i = 0; i < C::WPT; ++i) {
+      const int idx = tid + i * 256;
+      if ((C::W4 % 256) == 0 || idx < C::W4) wl[idx] = wreg[i];
+    }
+    float* xl = smem + buf * C::BUF + C::WSZ;
+    const float slope = a.in_slope;
+#pragma unroll
+    for (int i = 0; i < C::XPT; ++i) {
+      const int e = tid + i * 256;
+      if (e < C::XSZ) xl[e] = lrelu(xreg[i], slope);
+    }
+  };
+
+  f32x16 acc[U][TM][TN];
+#pragma unroll
+  for (int s = 0; s < U; ++s)
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[s][m][n] = f32x16{};
+
+  const int wcol = wm * TM * 32 + l32;
+  const int xcol = wn * TN * 32 + l32;
+
+  auto compute = [&](int buf) {
+    const float* wl = smem + buf * C::BUF;
+    const float* xl = wl + C::WSZ;
+#pragma unroll
+    for (int cp = 0; cp < CK / 2; ++cp) {
+      const int ci = 2 * cp + half;
+      float b0[TN], b1[TN];
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        b0[n] = xl[ci * C::XW + xcol + n * 32 + 1];  // x[m]
+        b1[n] = xl[ci * C::XW + xcol + n * 32];      // x[m-1]
+      }
+#pragma unroll
+      for (int s = 0; s < U; ++s) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          const float a0 = wl[(s * CK + ci) * BM + wcol + m * 32];
+          const float a1 = wl[((s + U) * CK + ci) * BM + wcol + m * 32];
+#pragma unroll
+          for (int n = 0; n < TN; ++n) {
+            acc[s][m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0[n], acc[s][m][n], 0, 0, 0);
+            acc[s][m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[n], acc[s][m][n], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+
+  const int nc = a.n_chunks;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  for (int c = 0; c < nc; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nc) load_chunk(c + 1);
+    compute(buf);
+    if (c + 1 < nc) store_chunk(buf ^ 1);
+    __syncthreads();
+  }
+
+  const int Cout = a.Cout;
+  constexpr int P = U / 2;
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int mm = m0 + wn * TN * 32 + n * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = mt * BM + wm * TM * 32 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (co >= Cout || mm > Tin) continue;
+        const float bb = a.bias[co];
+        float* yrow = a.y + ((size_t)b * Cout + co) * Tout;
+        if constexpr (U == 8) {
+          // phases 0..3 -> t = 8mm-4 .. 8mm-1 ; phases 4..7 -> t = 8mm .. 8mm+3
+          if (mm >= 1) {
+            f32x4 v = {acc[0][m][n][r] + bb, acc[1][m][n][r] + bb, acc[2][m][n][r] + bb,
+                       acc[3][m][n][r] + bb};
+            *reinterpret_cast<f32x4*>(yrow + 8 * mm - 4) = v;
+          }
+          if (mm < Tin) {
+            f32x4 v = {acc[4][m][n][r] + bb, acc[5][m][n][r] + bb, acc[6][m][n][r] + bb,
+                       acc[7][m][n][r] + bb};
+            *reinterpret_cast<f32x4*>(yrow + 8 * mm) = v;
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < U; ++s) {
+            const int t = U * mm + s - P;
+            if (t >= 0 && t < Tout) yrow[t] = acc[s][m][n][r] + bb;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Tail: y = tanh(b + sum_ci sum_k w[ci][k] * lrelu(z[ci][t+k-3], slope)), one output per thread.
+// ---------------------------------------------------------------------------------------
+constexpr int POST_T = 256;
+constexpr int POST_K = 7;
+
+__global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float psmem[];
+  const int Cin = a.Cin;
+  const int T = a.T;
+  constexpr int XW = POST_T + POST_K - 1;
+  float* zs = psmem;                 // [Cin][XW]
+  float* ws = psmem + Cin * XW;      // [Cin][7]
+  const int tid = threadIdx.x;
+  const int t0 = blockIdx.x * POST_T;
+  const int b = blockIdx.y;
+  const float* zb = a.z + (size_t)b * Cin * T;
+  for (int e = tid; e < Cin * XW; e += 256) {
+    const int r = e / XW;
+    const int col = e - r * XW;
+    const int ts = t0 - (POST_K / 2) + col;
+    float v = 0.f;
+    if (ts >= 0 && ts < T) v = lrelu(zb[(size_t)r * T + ts], a.in_slope);
+    zs[e] = v;
+  }
+  for (int e = tid; e < Cin * POST_K; e += 256) ws[e] = a.w[e];
+  __syncthreads();
+  const int t = t0 + tid;
+  if (t < T) {
+    float acc = a.bias;
+    for (int ci = 0; ci < Cin; ++ci) {
+#pragma unroll
+      for (int k = 0; k < POST_K; ++k) acc = fmaf(ws[ci * POST_K + k], zs[ci * XW + tid + k], acc);
+    }
+    a.y[(size_t)b * T + t] = tanhf(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const float* Wc, const float* bc,
+                                                     float* cvec, int B, int Cc, int C0) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C0) return;
+  const int b = i / C0, co = i - b * C0;
+  float acc = 0.f;
+  for (int k = 0; k < Cc; ++k) acc = fmaf(Wc[(size_t)co * Cc + k], g[(size_t)b * Cc + k], acc);
+  cvec[i] = acc + bc[co];
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr ConvTile kConvTiles[] = {
+    {128, 128, 2, 2, 8},  // Cout > 64
+    {64, 256, 2, 2, 8},   // 32 < Cout <= 64
+    {32, 512, 1, 4, 8},   // Cout <= 32
+};
+
+template <int K, int BM, int BN, int TM, int TN, int CK>
+void launch_conv1d_t(const Conv1dArgs& a, int B, hipStream_t s) {
+  dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
+  const int halo = (K - 1) * a.dil;
+  if (halo <= (K - 1) * DMAX)
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, CK, (K - 1) * DMAX>), grid, dim3(256), 0, s, a);
+  else if (halo <= HALO_WIDE)
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, CK, HALO_WIDE>), grid, dim3(256), 0, s, a);
+  else
+    throw Error(3, "conv1d: (kernel_size-1)*dilation = " + std::to_string(halo) + " exceeds " +
+                       std::to_string(HALO_WIDE));
+}
+
+template <int K>
+void launch_conv1d_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
+  switch (tile) {
+    case 0: launch_conv1d_t<K, 128, 128, 2, 2, 8>(a, B, s); break;
+    case 1: launch_conv1d_t<K, 64, 256, 2, 2, 8>(a, B, s); break;
+    case 2: launch_conv1d_t<K, 32, 512, 1, 4, 8>(a, B, s); break;
+    default: throw Error(3, "conv1d: bad tile index");
+  }
+}
+
+// convT tiles: index by (U, Cout class)
+template <int U>
+struct ConvTTiles;
+template <>
+struct ConvTTiles<8> {
+  static constexpr ConvTile t[] = {{64, 64, 1, 1, 8}, {32, 128, 1, 1, 8}};
+};
+template <>
+struct ConvTTiles<4> {
+  static constexpr ConvTile t[] = {{64, 128, 1, 2, 8}, {32, 256, 1, 2, 8}};
+};
+template <>
+struct ConvTTiles<2> {
+  static constexpr ConvTile t[] = {{64, 256, 2, 2, 8}, {32, 512, 1, 4, 8}};
+};
+
+template <int U, int BM, int BN, int TM, int TN, int CK>
+void launch_convT_t(const ConvTArgs& a, int B, hipStream_t s) {
+  dim3 grid(ceil_div(a.Tin + 1, BN), ceil_div(a.Cout, BM), B);
+  hipLaunchKernelGGL((convT_mfma_kernel<U, BM, BN, TM, TN, CK>), grid, dim3(256), 0, s, a);
+}
+}  // namespace
+
+int conv1d_tile_for(int Cout, int /*K*/) {
+  if (Cout > 64) return 0;
+  if (Cout > 32) return 1;
+  return 2;
+}
+
+ConvTile conv1d_tile(int idx) {
+  TTS_REQUIRE(idx >= 0 && idx < 3, 3, "conv1d: bad tile index");
+  return kConvTiles[idx];
+}
+
+void launch_conv1d(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  switch (K) {
+    case 1: launch_conv1d_k<1>(a, B, tile, s); break;
+    case 3: launch_conv1d_k<3>(a, B, tile, s); break;
+    case 5: launch_conv1d_k<5>(a, B, tile, s); break;
+    case 7: launch_conv1d_k<7>(a, B, tile, s); break;
+    case 11: launch_conv1d_k<11>(a, B, tile, s); break;
+    default: throw Error(3, "conv1d: kernel size " + std::to_string(K) + " not supported (1,3,5,7,11)");
+  }
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+int convT_tile_for(int Cout, int /*U*/) { return Cout > 32 ? 0 : 1; }
+
+ConvTile convT_tile(int idx, int U) {
+  TTS_REQUIRE(idx == 0 || idx == 1, 3, "convT: bad tile index");
+  switch (U) {
+    case 8: return ConvTTiles<8>::t[idx];
+    case 4: return ConvTTiles<4>::t[idx];
+    case 2: return ConvTTiles<2>::t[idx];
+    default: throw Error(3, "ConvTranspose1d stride " + std::to_string(U) + " not supported (2,4,8)");
+  }
+}
+
+void launch_convT(const ConvTArgs& a, int B, int U, int tile, hipStream_t s) {
+  switch (U) {
+    case 8:
+      if (tile == 0) launch_convT_t<8, 64, 64, 1, 1, 8>(a, B, s);
+      else launch_convT_t<8, 32, 128, 1, 1, 8>(a, B, s);
+      break;
+    case 4:
+      if (tile == 0) launch_convT_t<4, 64, 128, 1, 2, 8>(a, B, s);
+      else launch_convT_t<4, 32, 256, 1, 2, 8>(a, B, s);
+      break;
+    case 2:
+      if (tile == 0) launch_convT_t<2, 64, 256, 2, 2, 8>(a, B, s);
+      else launch_convT_t<2, 32, 512, 1, 4, 8>(a, B, s);
+      break;
+    default: throw Error(3, "ConvTranspose1d stride " + std::to_string(U) + " not supported (2,4,8)");
+  }
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
+  const size_t lds = (size_t)a.Cin * (POST_T + POST_K - 1 + POST_K) * sizeof(float);
+  TTS_REQUIRE(lds <= 64 * 1024, 3, "conv_post: too many input channels");
+  dim3 grid(ceil_div(a.T, POST_T), B);
+  hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), lds, s, a);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
+                     int C0, hipStream_t s) {
+  hipLaunchKernelGGL(cond_vec_kernel, dim3(ceil_div(B * C0, 256)), dim3(256), 0, s, g, Wc, bc, cvec, B,
+                     Cc, C0);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tts

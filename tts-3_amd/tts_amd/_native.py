@@ -1,0 +1,189 @@
+"""ctypes binding of ``libtts_mi355x.so`` (the C-ABI in ``include/tts_mi355x.h``).
+
+The library is the only compute path of this package: there is no CPU or PyTorch fallback.
+If the shared object is missing or fails to load, every entry point raises.
+
+``torch`` is imported before the library is opened so that the library's ``DT_NEEDED``
+``libamdhip64.so.7`` binds to the HIP runtime PyTorch already loaded (one runtime per process:
+device pointers and streams from PyTorch are then valid inside the library).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char, c_char_p, c_double, c_float, c_int, c_int64, c_void_p
+
+import torch  # noqa: F401  (load order: see module docstring)
+
+_LIB_NAME = "libtts_mi355x.so"
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+LIB_PATH = os.environ.get("TTS_MI355X_LIB", os.path.join(_LIB_DIR, _LIB_NAME))
+
+TTS_OK = 0
+TTS_ERR_INVALID = 1
+TTS_ERR_HIP = 2
+TTS_ERR_UNSUPPORTED = 3
+TTS_ERR_OOM = 4
+
+MAX_UPSAMPLES = 8
+MAX_KERNELS = 4
+MAX_DILATIONS = 4
+
+
+class TtsHifiganCfg(Structure):
+    _fields_ = [
+        ("in_channels", c_int),
+        ("out_channels", c_int),
+        ("resblock_type", c_int),
+        ("num_kernels", c_int),
+        ("resblock_kernel_sizes", c_int * MAX_KERNELS),
+        ("num_dilations", c_int),
+        ("resblock_dilation_sizes", (c_int * MAX_DILATIONS) * MAX_KERNELS),
+        ("num_upsamples", c_int),
+        ("upsample_factors", c_int * MAX_UPSAMPLES),
+        ("upsample_kernel_sizes", c_int * MAX_UPSAMPLES),
+        ("upsample_initial_channel", c_int),
+        ("inference_padding", c_int),
+        ("cond_channels", c_int),
+        ("conv_post_bias", c_int),
+    ]
+
+
+class TtsGlowDecoderCfg(Structure):
+    _fields_ = [
+        ("in_channels", c_int),
+        ("hidden_channels", c_int),
+        ("kernel_size", c_int),
+        ("dilation_rate", c_int),
+        ("num_flow_blocks", c_int),
+        ("num_coupling_layers", c_int),
+        ("num_splits", c_int),
+        ("num_squeeze", c_int),
+        ("sigmoid_scale", c_int),
+        ("c_in_channels", c_int),
+    ]
+
+
+class TtsLaunchRecord(Structure):
+    _fields_ = [("name", c_char * 48), ("flops", c_double), ("bytes", c_double), ("ms", c_float)]
+
+
+class TtsConv1dDesc(Structure):
+    _fields_ = [
+        ("B", c_int),
+        ("Cin", c_int),
+        ("Cout", c_int),
+        ("Tin", c_int),
+        ("K", c_int),
+        ("dil", c_int),
+        ("rep_pad", c_int),
+        ("in_slope", c_float),
+        ("out_slope", c_float),
+        ("zmode", c_int),
+        ("zdiv", c_float),
+    ]
+
+
+# name -> (restype, argtypes); must list every function declared in include/tts_mi355x.h
+SIGNATURES = {
+    "tts_last_error": (c_char_p, []),
+    "tts_abi_version": (c_int, []),
+    "tts_build_target": (c_char_p, []),
+    "tts_hifigan_num_weights": (c_int, [POINTER(TtsHifiganCfg)]),
+    "tts_hifigan_weight_numel": (c_int64, [POINTER(TtsHifiganCfg), c_int]),
+    "tts_hifigan_create": (c_int, [POINTER(TtsHifiganCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
+    "tts_hifigan_destroy": (c_int, [c_void_p]),
+    "tts_hifigan_output_length": (c_int64, [c_void_p, c_int, c_int]),
+    "tts_hifigan_workspace_bytes": (c_int64, [c_void_p, c_int, c_int, c_int]),
+    "tts_hifigan_reserve": (c_int, [c_void_p, c_int, c_int, c_int]),
+    "tts_hifigan_forward": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    ),
+    "tts_hifigan_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_glow_decoder_num_weights": (c_int, [POINTER(TtsGlowDecoderCfg)]),
+    "tts_glow_decoder_weight_numel": (c_int64, [POINTER(TtsGlowDecoderCfg), c_int]),
+    "tts_glow_decoder_create": (
+        c_int, [POINTER(TtsGlowDecoderCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]
+    ),
+    "tts_glow_decoder_destroy": (c_int, [c_void_p]),
+    "tts_glow_decoder_forward": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]
+    ),
+    "tts_op_conv1d": (
+        c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    ),
+    "tts_op_conv_transpose1d": (
+        c_int,
+        [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p],
+    ),
+    "tts_op_conv_post": (
+        c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]
+    ),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    """A C-ABI call returned a non-zero status."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed (status {code}): {msg}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Open the library (once).  Raises if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{_LIB_NAME} not found at {LIB_PATH}: build it with `make -C tts-3_amd` "
+            "(or __graft_entry__.build()); the MI355X path has no CPU fallback"
+        )
+    handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = handle
+    return _lib
+
+
+def check(fn_name: str, status: int) -> None:
+    if status != TTS_OK:
+        msg = lib().tts_last_error().decode(errors="replace")
+        raise NativeError(fn_name, status, msg)
+
+
+def call(fn_name: str, *args) -> int:
+    """Call a status-returning entry point and raise on failure."""
+    st = getattr(lib(), fn_name)(*args)
+    check(fn_name, st)
+    return st
+
+
+def ptr(t) -> c_void_p:
+    """Raw device/host pointer of a tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return c_void_p(0)
+    if hasattr(t, "data_ptr"):
+        return c_void_p(t.data_ptr())
+    return c_void_p(t.ctypes.data)
+
+
+def stream_ptr(device: torch.device) -> c_void_p:
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device_tensor(t: torch.Tensor, what: str) -> None:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what} must be a ROCm device tensor: the tts_amd path runs only on MI355X (no CPU fallback)"
+        )

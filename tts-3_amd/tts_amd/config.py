@@ -1,0 +1,39 @@
+"""Configuration defaults of the two reference modules this package replaces, and a plain
+JSON reader (no coqpit dependency).
+
+* ``HIFIGAN_V1``: ``HifiganConfig.generator_model_params`` (TTS/vocoder/configs/hifigan_config.py:95-104)
+* ``GLOW_TTS_DECODER``: the decoder fields of ``GlowTTSConfig`` (TTS/tts/configs/glow_tts_config.py:117-131)
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict
+
+HIFIGAN_V1: Dict[str, Any] = {
+    "upsample_factors": [8, 8, 2, 2],
+    "upsample_kernel_sizes": [16, 16, 4, 4],
+    "upsample_initial_channel": 512,
+    "resblock_kernel_sizes": [3, 7, 11],
+    "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+    "resblock_type": "1",
+}
+
+GLOW_TTS_DECODER: Dict[str, Any] = {
+    "in_channels": 80,          # out_channels
+    "hidden_channels": 192,     # hidden_channels_dec
+    "kernel_size": 5,           # kernel_size_dec
+    "dilation_rate": 1,
+    "num_flow_blocks": 12,      # num_flow_blocks_dec
+    "num_coupling_layers": 4,   # num_block_layers
+    "dropout_p": 0.05,          # dropout_p_dec (identity at inference)
+    "num_splits": 4,
+    "num_squeeze": 2,
+    "sigmoid_scale": False,
+    "c_in_channels": 0,
+}
+
+
+def load_config(path: str) -> Dict[str, Any]:
+    """Read a Coqui JSON config (``TTS/config/__init__.py:68-100`` reads the same files)."""
+    with open(path, "r", encoding="utf-8") as f:
+        return json.load(f)

@@ -1,0 +1,171 @@
+"""Deterministic synthetic checkpoints with the reference's state_dict keys.
+
+There are no pretrained HiFiGAN / Glow-TTS checkpoints offline, and PyTorch's default init
+makes HiFiGAN's output nearly constant (std ~0.002), which is a weak parity test.  These
+generators draw variance-preserving weights from ``numpy.random.default_rng(seed)`` in a fixed
+key order:
+
+* Conv1d weight  ~ N(0,1) * s / sqrt(Cin*k), s = 0.5 on the C->C MRF convs, 1 elsewhere
+* ConvTranspose1d weight ~ N(0,1) / sqrt(Cin*k/u)
+* biases ~ N(0, 0.01^2)
+* weight norm: v = the weight above, g = ||v|| * exp(0.1*N(0,1)) per output channel (dim 0),
+  so folding g*v/||v|| is exercised with non-trivial g.
+
+Keys match ``TTS/vocoder/models/hifigan_generator.py`` (torch.nn.utils.parametrizations
+.weight_norm naming: ``<conv>.parametrizations.weight.original0`` = g,
+``original1`` = v) and ``TTS/tts/layers/glow_tts/decoder.py``.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from .config import HIFIGAN_V1, GLOW_TTS_DECODER
+
+
+def _wn_pair(rng, v: np.ndarray):
+    dims = tuple(range(1, v.ndim))
+    norm = np.sqrt((v.astype(np.float64) ** 2).sum(axis=dims, keepdims=True))
+    g = norm * np.exp(0.1 * rng.standard_normal(norm.shape))
+    return g.astype(np.float32), v.astype(np.float32)
+
+
+def hifigan_state_dict(
+    in_channels: int = 80,
+    out_channels: int = 1,
+    resblock_type: str = "1",
+    resblock_dilation_sizes: Sequence[Sequence[int]] = HIFIGAN_V1["resblock_dilation_sizes"],
+    resblock_kernel_sizes: Sequence[int] = HIFIGAN_V1["resblock_kernel_sizes"],
+    upsample_kernel_sizes: Sequence[int] = HIFIGAN_V1["upsample_kernel_sizes"],
+    upsample_initial_channel: int = HIFIGAN_V1["upsample_initial_channel"],
+    upsample_factors: Sequence[int] = HIFIGAN_V1["upsample_factors"],
+    cond_channels: int = 0,
+    conv_pre_weight_norm: bool = True,
+    conv_post_weight_norm: bool = True,
+    conv_post_bias: bool = True,
+    seed: int = 1234,
+    weight_norm: bool = True,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a HifiganGenerator (hifigan_generator.py:163-234) with synthetic weights.
+
+    ``weight_norm=True`` gives the training-time parametrized keys; ``False`` gives the keys
+    after ``remove_weight_norm`` (plain ``.weight``).
+    """
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    C0 = upsample_initial_channel
+
+    def conv(name: str, cout: int, cin: int, k: int, scale: float, wn: bool, bias: bool = True,
+             fan: float = None):
+        fan = cin * k if fan is None else fan
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(fan))
+        b = rng.standard_normal((cout,)) * 0.01 if bias else None
+        if b is not None:
+            sd[f"{name}.bias"] = torch.from_numpy(b.astype(np.float32))
+        if wn and weight_norm:
+            g, v = _wn_pair(rng, w)
+            sd[f"{name}.parametrizations.weight.original0"] = torch.from_numpy(g)
+            sd[f"{name}.parametrizations.weight.original1"] = torch.from_numpy(v)
+        else:
+            if wn:  # consume the same random stream as the parametrized variant
+                g, v = _wn_pair(rng, w)
+                w = (g / np.sqrt((v.astype(np.float64) ** 2).sum(axis=(1, 2), keepdims=True))) * v
+            sd[f"{name}.weight"] = torch.from_numpy(np.ascontiguousarray(w, dtype=np.float32))
+
+    def convT(name: str, cin: int, cout: int, k: int, u: int):
+        w = rng.standard_normal((cin, cout, k)) / np.sqrt(cin * k / u)
+        b = rng.standard_normal((cout,)) * 0.01
+        sd[f"{name}.bias"] = torch.from_numpy(b.astype(np.float32))
+        g, v = _wn_pair(rng, w)
+        if weight_norm:
+            sd[f"{name}.parametrizations.weight.original0"] = torch.from_numpy(g)
+            sd[f"{name}.parametrizations.weight.original1"] = torch.from_numpy(v)
+        else:
+            wf = (g / np.sqrt((v.astype(np.float64) ** 2).sum(axis=(1, 2), keepdims=True))) * v
+            sd[f"{name}.weight"] = torch.from_numpy(wf.astype(np.float32))
+
+    conv("conv_pre", C0, in_channels, 7, 1.0, conv_pre_weight_norm)
+    for i, (u, k) in enumerate(zip(upsample_factors, upsample_kernel_sizes)):
+        convT(f"ups.{i}", C0 >> i, C0 >> (i + 1), k, u)
+    r = 0
+    for i in range(len(upsample_factors)):
+        ch = C0 >> (i + 1)
+        for k, dil in zip(resblock_kernel_sizes, resblock_dilation_sizes):
+            if resblock_type == "1":
+                for m in range(3):
+                    conv(f"resblocks.{r}.convs1.{m}", ch, ch, k, 0.5, True)
+                for m in range(3):
+                    conv(f"resblocks.{r}.convs2.{m}", ch, ch, k, 0.5, True)
+            else:
+                for m in range(2):
+                    conv(f"resblocks.{r}.convs.{m}", ch, ch, k, 0.5, True)
+            r += 1
+    ch = C0 >> len(upsample_factors)
+    conv("conv_post", out_channels, ch, 7, 1.0, conv_post_weight_norm, bias=conv_post_bias)
+    if cond_channels > 0:
+        w = rng.standard_normal((C0, cond_channels, 1)) / np.sqrt(cond_channels)
+        sd["cond_layer.weight"] = torch.from_numpy(w.astype(np.float32))
+        sd["cond_layer.bias"] = torch.from_numpy((rng.standard_normal((C0,)) * 0.01).astype(np.float32))
+    # canonical module order: conv_pre, ups, resblocks, conv_post, cond_layer
+    return sd
+
+
+def glow_decoder_state_dict(
+    in_channels: int = GLOW_TTS_DECODER["in_channels"],
+    hidden_channels: int = GLOW_TTS_DECODER["hidden_channels"],
+    kernel_size: int = GLOW_TTS_DECODER["kernel_size"],
+    dilation_rate: int = GLOW_TTS_DECODER["dilation_rate"],
+    num_flow_blocks: int = GLOW_TTS_DECODER["num_flow_blocks"],
+    num_coupling_layers: int = GLOW_TTS_DECODER["num_coupling_layers"],
+    num_splits: int = GLOW_TTS_DECODER["num_splits"],
+    num_squeeze: int = GLOW_TTS_DECODER["num_squeeze"],
+    seed: int = 4321,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a Glow-TTS ``Decoder`` (decoder.py:68-111) with synthetic weights.
+
+    ``end`` (zero-initialised in the reference, glow.py:194-196) and ActNorm are randomised too,
+    otherwise the reverse flow is an identity map and parity says nothing.
+    """
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    C2 = in_channels * num_squeeze
+    H = hidden_channels
+    S = num_splits
+
+    def wn_conv(name: str, cout: int, cin: int, k: int, scale: float):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        b = rng.standard_normal((cout,)) * 0.02
+        sd[f"{name}.bias"] = torch.from_numpy(b.astype(np.float32))
+        g, v = _wn_pair(rng, w)
+        sd[f"{name}.parametrizations.weight.original0"] = torch.from_numpy(g)
+        sd[f"{name}.parametrizations.weight.original1"] = torch.from_numpy(v)
+
+    for f in range(num_flow_blocks):
+        a, c, cb = 3 * f, 3 * f + 1, 3 * f + 2
+        sd[f"flows.{a}.logs"] = torch.from_numpy((rng.standard_normal((1, C2, 1)) * 0.1).astype(np.float32))
+        sd[f"flows.{a}.bias"] = torch.from_numpy((rng.standard_normal((1, C2, 1)) * 0.1).astype(np.float32))
+        q, _ = np.linalg.qr(rng.standard_normal((S, S)))
+        if np.linalg.det(q) < 0:
+            q[:, 0] = -q[:, 0]
+        sd[f"flows.{c}.weight"] = torch.from_numpy(np.ascontiguousarray(q, dtype=np.float32))
+        wn_conv(f"flows.{cb}.start", H, C2 // 2, 1, 1.0)
+        w_end = rng.standard_normal((C2, H, 1)) * (0.1 / np.sqrt(H))
+        sd[f"flows.{cb}.end.weight"] = torch.from_numpy(w_end.astype(np.float32))
+        sd[f"flows.{cb}.end.bias"] = torch.from_numpy((rng.standard_normal((C2,)) * 0.02).astype(np.float32))
+        for l in range(num_coupling_layers):
+            wn_conv(f"flows.{cb}.wn.in_layers.{l}", 2 * H, H, kernel_size, 1.0)
+        for l in range(num_coupling_layers):
+            rsc = 2 * H if l < num_coupling_layers - 1 else H
+            wn_conv(f"flows.{cb}.wn.res_skip_layers.{l}", rsc, H, 1, 1.0)
+    return sd
+
+
+def mel(batch: int, frames: int, channels: int = 80, seed: int = 0) -> torch.Tensor:
+    """Synthetic N(0,1) mel [B, C, T] (torch generator, CPU)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(batch, channels, frames, generator=g)

@@ -1,0 +1,61 @@
+"""Inference surface of ``TTS/vocoder/models/gan.py`` (``GAN``) and the generator factory of
+``TTS/vocoder/models/__init__.py``.  Training (discriminator, losses, train_step) is out of
+scope: this package accelerates the inference path only.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict
+
+import torch
+
+from ..io import load_fsspec
+from .hifigan_generator import HifiganGenerator
+
+
+def _get(c: Any, key: str, default=None):
+    if isinstance(c, dict):
+        return c.get(key, default)
+    return getattr(c, key, default)
+
+
+def setup_generator(c: Any) -> HifiganGenerator:
+    """``setup_generator`` (vocoder/models/__init__.py:34-41) for the HiFiGAN branch:
+    ``HifiganGenerator(in_channels=c.audio["num_mels"], out_channels=1, **c.generator_model_params)``."""
+    name = str(_get(c, "generator_model", "hifigan_generator")).lower()
+    if name not in "hifigan_generator":  # the reference's substring test (:40)
+        raise NotImplementedError(f"generator {name!r}: only hifigan_generator runs on the MI355X path")
+    audio = _get(c, "audio", {}) or {}
+    num_mels = audio["num_mels"] if isinstance(audio, dict) else audio.num_mels
+    params: Dict[str, Any] = dict(_get(c, "generator_model_params"))
+    return HifiganGenerator(in_channels=num_mels, out_channels=1, **params)
+
+
+class GAN(torch.nn.Module):
+    """``GAN`` wrapper, inference part (gan.py:22-66, :229-252, :371-374)."""
+
+    def __init__(self, config: Any):
+        super().__init__()
+        self.config = config
+        self.model_g = setup_generator(config)
+        self.model_d = None
+
+    @classmethod
+    def init_from_config(cls, config: Any) -> "GAN":
+        return cls(config)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:  # gan.py:47-56
+        return self.model_g.forward(x)
+
+    def inference(self, x: torch.Tensor) -> torch.Tensor:  # gan.py:58-66
+        return self.model_g.inference(x)
+
+    def load_checkpoint(self, config, checkpoint_path, eval=False, cache=False):  # noqa: A002  gan.py:229-252
+        state = load_fsspec(checkpoint_path, map_location=torch.device("cpu"), cache=cache)
+        if "model_disc" in state:  # band-aid for older than v0.0.15 GAN models
+            self.model_g.load_checkpoint(config, checkpoint_path, eval)
+            return
+        g_state = {k[len("model_g."):]: v for k, v in state["model"].items() if k.startswith("model_g.")}
+        self.model_g.load_state_dict(g_state)
+        if eval:
+            self.model_d = None
+            self.model_g.remove_weight_norm()
