@@ -15,6 +15,7 @@ Prints ONE JSON line (rank 0) with the driver contract fields plus:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -111,7 +112,8 @@ def main():
 
     cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
     g = HifiganGenerator(**cfg)
-    g.remove_weight_norm()
+    with contextlib.redirect_stdout(sys.stderr):  # the reference prints "Removing weight norm..."
+        g.remove_weight_norm()
     g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False))
     g.eval()
     g = g.to(dev)

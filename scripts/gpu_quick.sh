@@ -1,0 +1,13 @@
+# parity tests + bench (no CPU baseline) + per-kernel breakdown
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -le 1 ]; then
+  timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
+  echo "bench rc=$?"
+  python -c "import json;d=json.load(open('gpurun_out/bench.json'));print(d['value'],d['ms_per_step'],d['model_frac_fp32_peak']);print(d['roofline']);print(d['kernel_breakdown_ms'])"
+fi

@@ -95,7 +95,7 @@ void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cv
                      int C0, hipStream_t s);
 
 // Host-side weight packing (pack.cpp).
-// Conv1d torch weight [Cout][Cin][K] -> [Cout_pad/BM][n_chunks][K][CK][BM] (zero padded).
+// Conv1d torch weight [Cout][Cin][K] -> MFMA fragments [mblock32][cgroup8][K][64][4] (+slack).
 void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
 int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] -> [Cout_pad/BM][n_chunks][2U][CK][BM].

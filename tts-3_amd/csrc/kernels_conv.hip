@@ -21,31 +21,36 @@
 
 namespace tts {
 
-// Halo ((K-1)*dilation) the register-staged input window is sized for: the narrow variant
-// covers dilation <= 5 (HiFiGAN v1/v2, Glow WN), the wide one HiFiGAN-v3's dilation 6 / 12.
+// Halo ((K-1)*dilation) the staged input window is sized for: the narrow variant covers
+// dilation <= 5 (HiFiGAN v1/v2, Glow WN), the wide one HiFiGAN-v3's dilation 6 / 12.
 constexpr int DMAX = 5;
 constexpr int HALO_WIDE = 96;
 
-template <int K, int BM, int BN, int TM, int TN, int CK, int HMAX>
+// conv1d_mfma v2
+//   A operand (weights) is streamed from L2 straight into VGPRs: the host packs W into
+//   MFMA fragments [mblock32][cgroup8][tap][lane 64][4], so one coalesced 1 KiB dwordx4 per
+//   wave brings 4 k-substeps (8 input channels: lane half h holds channels 4h..4h+3) of one
+//   32-row block; prefetched one step ahead.
+//   B operand (input window) is staged once per chunk in LDS as [group][t][8 ch + 4 pad]:
+//   48-byte rows make the per-lane ds_read_b128 (4 k-substeps of one column) conflict-free
+//   at any tap shift k*dil.  The leaky_relu before the conv is applied while staging.
+//   One step = (channel group, tap): TM A-loads, TN b128 LDS reads, 4*TM*TN MFMAs.
+template <int K, int BM, int BN, int TM, int TN, int G, int HMAX>
 struct ConvCfg {
   static constexpr int WM = BM / (32 * TM);
   static constexpr int WN = BN / (32 * TN);
-  static constexpr int WSZ = K * CK * BM;  // floats in one weight chunk
-  static constexpr int W4 = WSZ / 4;
-  static constexpr int WPT = (W4 + 255) / 256;  // float4 per thread
-  static constexpr int XWMAX = BN + HMAX;
-  static constexpr int XSZ = CK * XWMAX;  // floats reserved for one input window
-  static constexpr int XPT = (XSZ + 255) / 256;
-  static constexpr int BUF = WSZ + XSZ;  // floats per LDS buffer (WSZ multiple of 4)
+  static constexpr int CK = 8 * G;               // input channels per LDS chunk
+  static constexpr int XROWS = BN + HMAX;        // t rows reserved per group
+  static constexpr int XSZ = G * XROWS * 12;     // floats per LDS buffer
+  static constexpr int UNITS = G * XROWS * 2;    // staging units (group, row, channel quad)
+  static constexpr int UPT = (UNITS + 255) / 256;
   static_assert(WM * WN == 4, "4 waves per workgroup");
-  static_assert(CK % 2 == 0, "MFMA depth is 2 channels");
-  static_assert(WSZ % 4 == 0, "");
 };
 
-template <int K, int BM, int BN, int TM, int TN, int CK, int HMAX>
+template <int K, int BM, int BN, int TM, int TN, int G, int HMAX>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
-  using C = ConvCfg<K, BM, BN, TM, TN, CK, HMAX>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * C::BUF];
+  using C = ConvCfg<K, BM, BN, TM, TN, G, HMAX>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::XSZ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -59,62 +64,73 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
   const int mt = blockIdx.y;
   const int b = blockIdx.z;
   const int d = a.dil;
-  const int XW = BN + (K - 1) * d;
-  const int xsz = CK * XW;
+  const int XW = BN + (K - 1) * d;  // rows actually used per group
   const int Tin = a.Tin;
   const int Tout = a.Tout;
+  const int Cin = a.Cin;
+  const int nc = a.n_chunks;
 
-  const float* __restrict__ xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)a.Cin * Tin);
-  const f32x4* __restrict__ wg = reinterpret_cast<const f32x4*>(a.w) + (size_t)mt * a.n_chunks * C::W4;
+  const float* __restrict__ xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
 
-  // Chunk-invariant part of this thread's input-window gather: element e = tid + i*256
-  // of the [CK][XW] window is row r, column col -> source offset r*Tin + clamp(ts - rep).
-  int xoff[C::XPT];
-  int xrow[C::XPT];
+  // ---- staging units (chunk invariant): unit u -> group g, row r, channel quad q
+  int uoff[C::UPT];   // element offset of channel (8g+4q) at the clamped source time
+  int uch[C::UPT];    // channel index 8g+4q within the chunk, or huge when the row is invalid
+  int ulds[C::UPT];   // LDS float offset of the row's quad
 #pragma unroll
-  for (int i = 0; i < C::XPT; ++i) {
-    const int e = tid + i * 256;
-    const int r = e / XW;
-    const int col = e - r * XW;
-    const int ts = t0 - a.pad + col;  // position in the (replicate-)padded sequence
-    const bool ok = (e < xsz) && ts >= 0 && ts < Tout;
+  for (int i = 0; i < C::UPT; ++i) {
+    const int u = tid + i * 256;
+    const int q = u & 1;
+    const int rr = u >> 1;
+    const int g = rr / XW;
+    const int r = rr - g * XW;
+    const int ts = t0 - a.pad + r;
+    const bool ok = (g < G) && ts >= 0 && ts < Tout;
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
-    xoff[i] = r * Tin + src;
-    xrow[i] = ok ? r : 0x40000000;  // row index, or "never valid"
+    uoff[i] = (8 * g + 4 * q) * Tin + src;
+    uch[i] = ok ? 8 * g + 4 * q : 0x40000000;
+    ulds[i] = (g < G) ? (g * C::XROWS + r) * 12 + 4 * q : -1;
   }
 
-  f32x4 wreg[C::WPT];
-  float xreg[C::XPT];
-
-  auto load_chunk = [&](int c) {
-    const f32x4* wc = wg + (size_t)c * C::W4;
+  f32x4 xreg[C::UPT];
+  auto load_x = [&](int c) {
+    const int c0 = c * C::CK;
+    const float* xc = xb + (size_t)c0 * Tin;
 #pragma unroll
-    for (int i = 0; i < C::WPT; ++i) {
-      const int idx = tid + i * 256;
-      if ((C::W4 % 256) == 0 || idx < C::W4) wreg[i] = wc[idx];
+    for (int i = 0; i < C::UPT; ++i) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = uch[i] + j;                       // channel within chunk
+        const bool ok = (c0 + ch) < Cin;
+        const int off = ok ? uoff[i] + j * Tin : 0;      // always in bounds
+        const float x = xc[off];
+        v[j] = ok ? x : 0.f;
+      }
+      xreg[i] = f32x4{v[0], v[1], v[2], v[3]};
     }
-    const int rows_left = a.Cin - c * CK;  // rows of this chunk that exist
-    const float* xc = xb + (size_t)c * CK * Tin;
-#pragma unroll
-    for (int i = 0; i < C::XPT; ++i) xreg[i] = (xrow[i] < rows_left) ? xc[xoff[i]] : 0.f;
   };
-
-  auto store_chunk = [&](int buf) {
-    f32x4* wl = reinterpret_cast<f32x4*>(smem + buf * C::BUF);
-#pragma unroll
-    for (int i = 0; i < C::WPT; ++i) {
-      const int idx = tid + i * 256;
-      if ((C::W4 % 256) == 0 || idx < C::W4) wl[idx] = wreg[i];
-    }
-    float* xl = smem + buf * C::BUF + C::WSZ;
+  auto store_x = [&](int buf) {
+    float* xl = smem + buf * C::XSZ;
     const float slope = a.in_slope;
 #pragma unroll
-    for (int i = 0; i < C::XPT; ++i) {
-      const int e = tid + i * 256;
-      if (e < xsz) xl[e] = lrelu(xreg[i], slope);
+    for (int i = 0; i < C::UPT; ++i) {
+      if (ulds[i] >= 0) {
+        f32x4 v = xreg[i];
+        v[0] = lrelu(v[0], slope); v[1] = lrelu(v[1], slope);
+        v[2] = lrelu(v[2], slope); v[3] = lrelu(v[3], slope);
+        *reinterpret_cast<f32x4*>(xl + ulds[i]) = v;
+      }
     }
   };
+
+  // ---- A fragment streams: one per m-block of this wave, step index = c8 * K + k
+  const f32x4* ap[TM];
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const int mb = mt * (BM / 32) + wm * TM + m;
+    ap[m] = reinterpret_cast<const f32x4*>(a.w) + ((size_t)mb * nc * G * K) * 64 + lane;
+  }
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -122,40 +138,59 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
 #pragma unroll
     for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
 
-  const int wcol = wm * TM * 32 + l32;          // A: output-channel lane offset
-  const int xcol = wn * TN * 32 + l32;          // B: output-time lane offset
+  const int xrow0 = wn * TN * 32 + l32;  // B: this lane's output column within the tile
 
-  auto compute = [&](int buf) {
-    const float* wl = smem + buf * C::BUF;
-    const float* xl = wl + C::WSZ;
+  f32x4 acur[TM], anext[TM], bcur[TN], bnext[TN];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-      for (int cp = 0; cp < CK / 2; ++cp) {
-        const int ci = 2 * cp + half;
-        float av[TM], bv[TN];
-#pragma unroll
-        for (int m = 0; m < TM; ++m) av[m] = wl[(k * CK + ci) * BM + wcol + m * 32];
-#pragma unroll
-        for (int n = 0; n < TN; ++n) bv[n] = xl[ci * XW + xcol + n * 32 + k * d];
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-      }
-    }
-  };
+  for (int m = 0; m < TM; ++m) acur[m] = ap[m][0];
 
-  const int nc = a.n_chunks;
-  load_chunk(0);
-  store_chunk(0);
+  load_x(0);
+  store_x(0);
   __syncthreads();
+
   for (int c = 0; c < nc; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nc) load_chunk(c + 1);
-    compute(buf);
-    if (c + 1 < nc) store_chunk(buf ^ 1);
+    const float* xl = smem + buf * C::XSZ + 4 * half;
+    const bool more = c + 1 < nc;
+    if (more) load_x(c + 1);
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+      bcur[n] = *reinterpret_cast<const f32x4*>(xl + (xrow0 + n * 32) * 12);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int s = (c * G + g) * K + k;  // global step of this (group, tap)
+        // prefetch the next step: A from L2 (the stream is padded by one fragment), B from LDS
+#pragma unroll
+        for (int m = 0; m < TM; ++m) anext[m] = ap[m][(size_t)(s + 1) * 64];
+        const bool bnext_here = (k + 1 < K) || (g + 1 < G);
+        if (bnext_here) {
+          const int gn = (k + 1 < K) ? g : g + 1;
+          const int kn = (k + 1 < K) ? k + 1 : 0;
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            bnext[n] = *reinterpret_cast<const f32x4*>(xl + ((gn * C::XROWS) + xrow0 + n * 32 + kn * d) * 12);
+        }
+        // keep the prefetches ahead of this step's MFMAs (the scheduler otherwise sinks them
+        // to their use and exposes the L2 / LDS latency every step)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int n = 0; n < TN; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[m][j], bcur[n][j], acc[m][n], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < TM; ++m) acur[m] = anext[m];
+        if (bnext_here) {
+#pragma unroll
+          for (int n = 0; n < TN; ++n) bcur[n] = bnext[n];
+        }
+      }
+    }
+    if (more) store_x(buf ^ 1);
     __syncthreads();
   }
 
@@ -422,20 +457,21 @@ __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const flo
 // Host launchers
 // ---------------------------------------------------------------------------------------
 namespace {
+// {BM, BN, TM, TN, CK = 8*G}
 constexpr ConvTile kConvTiles[] = {
-    {128, 128, 2, 2, 8},  // Cout > 64
-    {64, 256, 2, 2, 8},   // 32 < Cout <= 64
-    {32, 512, 1, 4, 8},   // Cout <= 32
+    {128, 128, 2, 2, 16},  // Cout > 64
+    {64, 256, 2, 2, 16},   // 32 < Cout <= 64
+    {32, 512, 1, 4, 8},    // Cout <= 32
 };
 
-template <int K, int BM, int BN, int TM, int TN, int CK>
+template <int K, int BM, int BN, int TM, int TN, int G>
 void launch_conv1d_t(const Conv1dArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
   const int halo = (K - 1) * a.dil;
   if (halo <= (K - 1) * DMAX)
-    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, CK, (K - 1) * DMAX>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, (K - 1) * DMAX>), grid, dim3(256), 0, s, a);
   else if (halo <= HALO_WIDE)
-    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, CK, HALO_WIDE>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, HALO_WIDE>), grid, dim3(256), 0, s, a);
   else
     throw Error(3, "conv1d: (kernel_size-1)*dilation = " + std::to_string(halo) + " exceeds " +
                        std::to_string(HALO_WIDE));
@@ -444,9 +480,9 @@ void launch_conv1d_t(const Conv1dArgs& a, int B, hipStream_t s) {
 template <int K>
 void launch_conv1d_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: launch_conv1d_t<K, 128, 128, 2, 2, 8>(a, B, s); break;
-    case 1: launch_conv1d_t<K, 64, 256, 2, 2, 8>(a, B, s); break;
-    case 2: launch_conv1d_t<K, 32, 512, 1, 4, 8>(a, B, s); break;
+    case 0: launch_conv1d_t<K, 128, 128, 2, 2, 2>(a, B, s); break;
+    case 1: launch_conv1d_t<K, 64, 256, 2, 2, 2>(a, B, s); break;
+    case 2: launch_conv1d_t<K, 32, 512, 1, 4, 1>(a, B, s); break;
     default: throw Error(3, "conv1d: bad tile index");
   }
 }

@@ -6,26 +6,30 @@
 
 namespace tts {
 
+// MFMA-fragment layout of the conv1d A operand (see conv1d_mfma_kernel):
+//   out[mb][c8][k][lane][j] = w[mb*32 + (lane&31)][c8*8 + 4*(lane>>5) + j][k]
+// mb over ceil(Cout/BM)*BM/32 blocks, c8 over n_chunks*CK/8 groups (zero padded), plus one
+// trailing fragment of slack for the kernel's one-step-ahead prefetch.
 int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t) {
-  const int64_t mtiles = ceil_div(Cout, t.BM);
-  const int64_t chunks = ceil_div(Cin, t.CK);
-  return mtiles * chunks * K * t.CK * t.BM;
+  const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
+  const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 8);
+  return mblocks * groups * K * 256 + 256;
 }
 
-// torch Conv1d weight w[Cout][Cin][K] -> out[mt][c][k][ci_l][co_l]
 void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
-  const int mtiles = ceil_div(Cout, t.BM);
-  const int chunks = ceil_div(Cin, t.CK);
+  const int mblocks = ceil_div(Cout, t.BM) * (t.BM / 32);
+  const int groups = ceil_div(Cin, t.CK) * (t.CK / 8);
   int64_t o = 0;
-  for (int mt = 0; mt < mtiles; ++mt)
-    for (int c = 0; c < chunks; ++c)
+  for (int mb = 0; mb < mblocks; ++mb)
+    for (int c8 = 0; c8 < groups; ++c8)
       for (int k = 0; k < K; ++k)
-        for (int cl = 0; cl < t.CK; ++cl)
-          for (int ml = 0; ml < t.BM; ++ml) {
-            const int co = mt * t.BM + ml;
-            const int ci = c * t.CK + cl;
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 4; ++j) {
+            const int co = mb * 32 + (lane & 31);
+            const int ci = c8 * 8 + 4 * (lane >> 5) + j;
             out[o++] = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
           }
+  for (int i = 0; i < 256; ++i) out[o++] = 0.f;
 }
 
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t) {
