@@ -82,7 +82,7 @@ def cpu_baseline(budget_s: float):
             hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float32, **cfg)
             n += 1
             el = time.perf_counter() - t0
-            if el >= budget_s or n >= 50:
+            if el >= budget_s or n >= 1000:
                 break
     samples = n * B * 256 * (T + 10)
     return {
