@@ -179,6 +179,14 @@ typedef struct TtsConv1dDesc {
 int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
                   const float* d_res, float* d_y, float* d_z, void* hip_stream);
 
+/* Tuning: same computation with an explicit tile configuration (tile < 0: automatic), launched
+ * `reps` times; *ms receives the mean kernel time (hipEvents on hip_stream). */
+int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
+                        const float* d_res, float* d_y, float* d_z, int tile, int reps, float* ms,
+                        void* hip_stream);
+/* Number of conv1d tile configurations compiled into the library. */
+int tts_op_conv1d_num_tiles(void);
+
 /* y = conv_transpose1d(act_in(x), w[Cin][Cout][K], b, stride, padding=(K-stride)/2);
  * requires K == 2*stride (every HiFiGAN config). */
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,

@@ -192,33 +192,61 @@ int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask
 }
 
 // ----------------------------------------------------------------------------- single ops
+static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
+                           const float* d_res, float* d_y, float* d_z, int tile, int reps, float* ms,
+                           void* hip_stream) {
+  TTS_REQUIRE(d && d_x && h_w && h_b, 1, "NULL argument");
+  TTS_REQUIRE(d->B >= 1 && d->Cin >= 1 && d->Cout >= 1 && d->Tin >= 1 && d->K >= 1 && d->dil >= 1, 1,
+              "bad conv1d shape");
+  TTS_REQUIRE((d->K % 2) == 1, 3, "conv1d: only odd kernel sizes ('same' padding)");
+  TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
+  TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
+  if (tile < 0) tile = tts::conv1d_tile_for(d->Cout, d->K, d->Cin, d->dil, d_res != nullptr);
+  const tts::ConvTile t = tts::conv1d_tile(tile);
+  std::vector<float> packed(tts::packed_conv1d_numel(d->Cout, d->Cin, d->K, t));
+  tts::pack_conv1d(h_w, d->Cout, d->Cin, d->K, t, packed.data());
+  std::vector<float> bias((size_t)tts::ceil_div(d->Cout, t.BM) * t.BM, 0.f);
+  std::memcpy(bias.data(), h_b, sizeof(float) * d->Cout);
+  TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
+  tts::Conv1dArgs a{};
+  a.x = d_x; a.w = w.p; a.bias = b.p; a.res = d_res; a.y = d_y; a.z = d_z; a.cvec = nullptr;
+  a.Cin = d->Cin; a.Cout = d->Cout; a.Tin = d->Tin; a.Tout = d->Tin + 2 * d->rep_pad;
+  a.dil = d->dil; a.pad = d->dil * (d->K - 1) / 2; a.rep_pad = d->rep_pad;
+  a.n_chunks = tts::ceil_div(d->Cin, t.CK);
+  a.in_slope = d->in_slope; a.out_slope = d->out_slope; a.zmode = d->zmode; a.zdiv = d->zdiv;
+  auto s = static_cast<hipStream_t>(hip_stream);
+  if (reps <= 0) {
+    tts::launch_conv1d(a, d->B, d->K, tile, s);
+  } else {
+    tts::launch_conv1d(a, d->B, d->K, tile, s);  // warm-up
+    hipEvent_t e0, e1;
+    TTS_HIP_CHECK(hipEventCreate(&e0));
+    TTS_HIP_CHECK(hipEventCreate(&e1));
+    TTS_HIP_CHECK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) tts::launch_conv1d(a, d->B, d->K, tile, s);
+    TTS_HIP_CHECK(hipEventRecord(e1, s));
+    TTS_HIP_CHECK(hipEventSynchronize(e1));
+    float total = 0.f;
+    TTS_HIP_CHECK(hipEventElapsedTime(&total, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ms) *ms = total / reps;
+  }
+  TTS_HIP_CHECK(hipStreamSynchronize(s));
+}
+
 int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
                   const float* d_res, float* d_y, float* d_z, void* hip_stream) {
-  return guarded([&] {
-    TTS_REQUIRE(d && d_x && h_w && h_b, 1, "NULL argument");
-    TTS_REQUIRE(d->B >= 1 && d->Cin >= 1 && d->Cout >= 1 && d->Tin >= 1 && d->K >= 1 && d->dil >= 1, 1,
-                "bad conv1d shape");
-    TTS_REQUIRE((d->K % 2) == 1, 3, "conv1d: only odd kernel sizes ('same' padding)");
-    TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
-    TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
-    const int tile = tts::conv1d_tile_for(d->Cout, d->K);
-    const tts::ConvTile t = tts::conv1d_tile(tile);
-    std::vector<float> packed(tts::packed_conv1d_numel(d->Cout, d->Cin, d->K, t));
-    tts::pack_conv1d(h_w, d->Cout, d->Cin, d->K, t, packed.data());
-    std::vector<float> bias((size_t)tts::ceil_div(d->Cout, t.BM) * t.BM, 0.f);
-    std::memcpy(bias.data(), h_b, sizeof(float) * d->Cout);
-    TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
-    tts::Conv1dArgs a{};
-    a.x = d_x; a.w = w.p; a.bias = b.p; a.res = d_res; a.y = d_y; a.z = d_z; a.cvec = nullptr;
-    a.Cin = d->Cin; a.Cout = d->Cout; a.Tin = d->Tin; a.Tout = d->Tin + 2 * d->rep_pad;
-    a.dil = d->dil; a.pad = d->dil * (d->K - 1) / 2; a.rep_pad = d->rep_pad;
-    a.n_chunks = tts::ceil_div(d->Cin, t.CK);
-    a.in_slope = d->in_slope; a.out_slope = d->out_slope; a.zmode = d->zmode; a.zdiv = d->zdiv;
-    auto s = static_cast<hipStream_t>(hip_stream);
-    tts::launch_conv1d(a, d->B, d->K, tile, s);
-    TTS_HIP_CHECK(hipStreamSynchronize(s));
-  });
+  return guarded([&] { op_conv1d_impl(d, d_x, h_w, h_b, d_res, d_y, d_z, -1, 0, nullptr, hip_stream); });
 }
+
+int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
+                        const float* d_res, float* d_y, float* d_z, int tile, int reps, float* ms,
+                        void* hip_stream) {
+  return guarded([&] { op_conv1d_impl(d, d_x, h_w, h_b, d_res, d_y, d_z, tile, reps, ms, hip_stream); });
+}
+
+int tts_op_conv1d_num_tiles(void) { return tts::conv1d_num_tiles(); }
 
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
                             const float* h_b, int Cout, int K, int stride, float in_slope,

@@ -56,9 +56,10 @@ struct Conv1dArgs {
   float zdiv;
 };
 
-// Tile shape of one conv1d kernel instance.
+// Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
 struct ConvTile {
   int BM, BN, TM, TN, CK;
+  int PD = 1;
 };
 
 // Polyphase ConvTranspose1d, K == 2*U, padding U/2: every output phase s is a dense
@@ -83,8 +84,9 @@ struct PostArgs {
 };
 
 // Host-side launchers (kernels_conv.hip).
-int conv1d_tile_for(int Cout, int K);                 // index into conv1d tile table
+int conv1d_tile_for(int Cout, int K, int Cin, int dil, bool res);  // index into the tile table
 ConvTile conv1d_tile(int idx);
+int conv1d_num_tiles();
 void launch_conv1d(const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
 int convT_tile_for(int Cout, int U);
 ConvTile convT_tile(int idx, int U);

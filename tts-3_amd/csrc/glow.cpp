@@ -76,7 +76,7 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   };
   auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
     cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
-    cv.tile = conv1d_tile_for(Cout, K);
+    cv.tile = conv1d_tile_for(Cout, K, Cin, dil, false);
     const ConvTile t = conv1d_tile(cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
     const size_t n = packed_conv1d_numel(Cout, Cin, K, t);

@@ -92,10 +92,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const int C0 = cfg_.upsample_initial_channel;
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
-  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam) {
+  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res) {
     ConvLayer L;
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
-    L.tile = conv1d_tile_for(Cout, K);
+    L.tile = conv1d_tile_for(Cout, K, Cin, dil, res);
     const ConvTile t = conv1d_tile(L.tile);
     L.n_chunks = ceil_div(Cin, t.CK);
     L.w_numel = packed_conv1d_numel(Cout, Cin, K, t);
@@ -104,7 +104,7 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     return L;
   };
 
-  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre");
+  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre", false);
   src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
     ConvTLayer L;
@@ -131,14 +131,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         for (int m = 0; m < 3; ++m) { w1[m] = hw[wi]; b1[m] = hw[wi + 1]; wi += 2; }
         for (int m = 0; m < 3; ++m) { w2[m] = hw[wi]; b2[m] = hw[wi + 1]; wi += 2; }
         for (int m = 0; m < 3; ++m) {
-          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv"));
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false));
           src.push_back({w1[m], b1[m]});
-          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv"));
+          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true));
           src.push_back({w2[m], b2[m]});
         }
       } else {
         for (int m = 0; m < 2; ++m) {
-          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv"));
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", true));
           src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
         }
       }

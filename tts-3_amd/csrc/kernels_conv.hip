@@ -35,21 +35,30 @@ constexpr int HALO_WIDE = 96;
 //   48-byte rows make the per-lane ds_read_b128 (4 k-substeps of one column) conflict-free
 //   at any tap shift k*dil.  The leaky_relu before the conv is applied while staging.
 //   One step = (channel group, tap): TM A-loads, TN b128 LDS reads, 4*TM*TN MFMAs.
-template <int K, int BM, int BN, int TM, int TN, int G, int HMAX>
+template <int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
 struct ConvCfg {
   static constexpr int WM = BM / (32 * TM);
   static constexpr int WN = BN / (32 * TN);
   static constexpr int CK = 8 * G;               // input channels per LDS chunk
   static constexpr int XROWS = BN + HMAX;        // t rows reserved per group
-  static constexpr int XSZ = G * XROWS * 12;     // floats per LDS buffer
+  static constexpr int XSZ = G * XROWS * 8;      // floats per LDS buffer (32-byte rows)
   static constexpr int UNITS = G * XROWS * 2;    // staging units (group, row, channel quad)
   static constexpr int UPT = (UNITS + 255) / 256;
   static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(PD == 1 || PD == 2, "A prefetch distance");
 };
 
-template <int K, int BM, int BN, int TM, int TN, int G, int HMAX>
+// LDS float offset of channel quad q (0/1) of input row r in group g.  The quad index is
+// XOR-swizzled with bit 3 of the row: every ds_read_b128 lane group (16 lanes, rows
+// r0 + {0-3,12-15,20-27} or {4-11,16-19,28-31}) then hits 16 distinct 16-byte bank slots
+// for ANY row shift r0 (the tap offset k*dil), with no padding.
+__device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
+  return (g * xrows + r) * 8 + 4 * (q ^ ((r >> 3) & 1));
+}
+
+template <int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
-  using C = ConvCfg<K, BM, BN, TM, TN, G, HMAX>;
+  using C = ConvCfg<K, BM, BN, TM, TN, G, HMAX, PD>;
   __shared__ __attribute__((aligned(16))) float smem[2 * C::XSZ];
 
   const int tid = threadIdx.x;
@@ -89,7 +98,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
     uoff[i] = (8 * g + 4 * q) * Tin + src;
     uch[i] = ok ? 8 * g + 4 * q : 0x40000000;
-    ulds[i] = (g < G) ? (g * C::XROWS + r) * 12 + 4 * q : -1;
+    ulds[i] = (g < G) ? xlds_off(g, r, q, C::XROWS) : -1;
   }
 
   f32x4 xreg[C::UPT];
@@ -140,9 +149,21 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
 
   const int xrow0 = wn * TN * 32 + l32;  // B: this lane's output column within the tile
 
-  f32x4 acur[TM], anext[TM], bcur[TN], bnext[TN];
+  // A ring: ar[0] = current step, ar[1..PD] = in flight
+  f32x4 ar[PD + 1][TM], bcur[TN], bnext[TN];
 #pragma unroll
-  for (int m = 0; m < TM; ++m) acur[m] = ap[m][0];
+  for (int p = 0; p < PD; ++p)
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ar[p][m] = ap[m][(size_t)p * 64];
+
+  // B read of (group g, tap k) for this lane's TN columns; quad = lane half
+  auto read_b = [&](const float* xl, int g, int k, f32x4* dst) {
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int r = xrow0 + n * 32 + k * d;
+      dst[n] = *reinterpret_cast<const f32x4*>(xl + xlds_off(g, r, half, C::XROWS));
+    }
+  };
 
   load_x(0);
   store_x(0);
@@ -150,28 +171,20 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
 
   for (int c = 0; c < nc; ++c) {
     const int buf = c & 1;
-    const float* xl = smem + buf * C::XSZ + 4 * half;
+    const float* xl = smem + buf * C::XSZ;
     const bool more = c + 1 < nc;
     if (more) load_x(c + 1);
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-      bcur[n] = *reinterpret_cast<const f32x4*>(xl + (xrow0 + n * 32) * 12);
+    read_b(xl, 0, 0, bcur);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int s = (c * G + g) * K + k;  // global step of this (group, tap)
-        // prefetch the next step: A from L2 (the stream is padded by one fragment), B from LDS
+        // prefetch: A for step s+PD from L2 (the stream is padded), B for step s+1 from LDS
 #pragma unroll
-        for (int m = 0; m < TM; ++m) anext[m] = ap[m][(size_t)(s + 1) * 64];
+        for (int m = 0; m < TM; ++m) ar[PD][m] = ap[m][(size_t)(s + PD) * 64];
         const bool bnext_here = (k + 1 < K) || (g + 1 < G);
-        if (bnext_here) {
-          const int gn = (k + 1 < K) ? g : g + 1;
-          const int kn = (k + 1 < K) ? k + 1 : 0;
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-            bnext[n] = *reinterpret_cast<const f32x4*>(xl + ((gn * C::XROWS) + xrow0 + n * 32 + kn * d) * 12);
-        }
+        if (bnext_here) read_b(xl, (k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
         // keep the prefetches ahead of this step's MFMAs (the scheduler otherwise sinks them
         // to their use and exposes the L2 / LDS latency every step)
         __builtin_amdgcn_sched_barrier(0);
@@ -181,9 +194,11 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
           for (int m = 0; m < TM; ++m)
 #pragma unroll
             for (int n = 0; n < TN; ++n)
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[m][j], bcur[n][j], acc[m][n], 0, 0, 0);
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[0][m][j], bcur[n][j], acc[m][n], 0, 0, 0);
 #pragma unroll
-        for (int m = 0; m < TM; ++m) acur[m] = anext[m];
+        for (int p = 0; p < PD; ++p)
+#pragma unroll
+          for (int m = 0; m < TM; ++m) ar[p][m] = ar[p + 1][m];
         if (bnext_here) {
 #pragma unroll
           for (int n = 0; n < TN; ++n) bcur[n] = bnext[n];
@@ -457,33 +472,61 @@ __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const flo
 // Host launchers
 // ---------------------------------------------------------------------------------------
 namespace {
-// {BM, BN, TM, TN, CK = 8*G}
+// {BM, BN, TM, TN, CK = 8*G, PD}.  Tiles 0-2 are the defaults picked by conv1d_tile_for;
+// the rest are tuning candidates (scripts/tune_conv.py), narrow halo only.
 constexpr ConvTile kConvTiles[] = {
-    {128, 128, 2, 2, 16},  // Cout > 64
-    {64, 256, 2, 2, 16},   // 32 < Cout <= 64
-    {32, 512, 1, 4, 8},    // Cout <= 32
+    {128, 128, 2, 2, 16, 1},  // 0  Cout > 64
+    {64, 256, 2, 2, 16, 1},   // 1  32 < Cout <= 64
+    {32, 512, 1, 4, 8, 1},    // 2  Cout <= 32
+    {128, 128, 2, 2, 32, 1},  // 3
+    {128, 128, 2, 2, 16, 2},  // 4
+    {128, 256, 2, 4, 16, 1},  // 5
+    {64, 256, 2, 2, 32, 1},   // 6
+    {64, 512, 2, 4, 16, 1},   // 7
+    {32, 256, 1, 2, 16, 1},   // 8
+    {32, 512, 1, 4, 16, 1},   // 9
+    {64, 128, 2, 1, 16, 1},   // 10
+    {128, 128, 2, 2, 32, 2},  // 11
+    {64, 256, 2, 2, 16, 2},   // 12
+    {32, 256, 1, 2, 32, 1},   // 13
 };
+constexpr int kNumConvTiles = sizeof(kConvTiles) / sizeof(kConvTiles[0]);
 
-template <int K, int BM, int BN, int TM, int TN, int G>
+template <int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE>
 void launch_conv1d_t(const Conv1dArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
   const int halo = (K - 1) * a.dil;
-  if (halo <= (K - 1) * DMAX)
-    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, (K - 1) * DMAX>), grid, dim3(256), 0, s, a);
-  else if (halo <= HALO_WIDE)
-    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, HALO_WIDE>), grid, dim3(256), 0, s, a);
-  else
+  if (halo <= (K - 1) * DMAX) {
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, (K - 1) * DMAX, PD>), grid, dim3(256), 0, s, a);
+  } else if (WIDE && halo <= HALO_WIDE) {
+    hipLaunchKernelGGL((conv1d_mfma_kernel<K, BM, BN, TM, TN, G, WIDE ? HALO_WIDE : 0, PD>), grid, dim3(256), 0, s,
+                       a);
+  } else {
     throw Error(3, "conv1d: (kernel_size-1)*dilation = " + std::to_string(halo) + " exceeds " +
-                       std::to_string(HALO_WIDE));
+                       std::to_string(WIDE ? HALO_WIDE : (K - 1) * DMAX) + " for this tile");
+  }
 }
 
 template <int K>
 void launch_conv1d_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: launch_conv1d_t<K, 128, 128, 2, 2, 2>(a, B, s); break;
-    case 1: launch_conv1d_t<K, 64, 256, 2, 2, 2>(a, B, s); break;
-    case 2: launch_conv1d_t<K, 32, 512, 1, 4, 1>(a, B, s); break;
-    default: throw Error(3, "conv1d: bad tile index");
+    case 0: launch_conv1d_t<K, 128, 128, 2, 2, 2, 1, true>(a, B, s); break;
+    case 1: launch_conv1d_t<K, 64, 256, 2, 2, 2, 1, true>(a, B, s); break;
+    case 2: launch_conv1d_t<K, 32, 512, 1, 4, 1, 1, true>(a, B, s); break;
+    case 3: launch_conv1d_t<K, 128, 128, 2, 2, 4, 1, false>(a, B, s); break;
+    case 4: launch_conv1d_t<K, 128, 128, 2, 2, 2, 2, false>(a, B, s); break;
+    case 8: launch_conv1d_t<K, 32, 256, 1, 2, 2, 1, false>(a, B, s); break;
+    case 10: launch_conv1d_t<K, 64, 128, 2, 1, 2, 1, false>(a, B, s); break;
+    case 11: launch_conv1d_t<K, 128, 128, 2, 2, 4, 2, false>(a, B, s); break;
+#ifdef TTS_TUNING_TILES  // candidates that never won the round-1 sweep (scripts/tune_conv.py)
+    case 5: launch_conv1d_t<K, 128, 256, 2, 4, 2, 1, false>(a, B, s); break;
+    case 6: launch_conv1d_t<K, 64, 256, 2, 2, 4, 1, false>(a, B, s); break;
+    case 7: launch_conv1d_t<K, 64, 512, 2, 4, 2, 1, false>(a, B, s); break;
+    case 9: launch_conv1d_t<K, 32, 512, 1, 4, 2, 1, false>(a, B, s); break;
+    case 12: launch_conv1d_t<K, 64, 256, 2, 2, 2, 2, false>(a, B, s); break;
+    case 13: launch_conv1d_t<K, 32, 256, 1, 2, 4, 1, false>(a, B, s); break;
+#endif
+    default: throw Error(3, "conv1d: bad tile index " + std::to_string(tile));
   }
 }
 
@@ -510,16 +553,25 @@ void launch_convT_t(const ConvTArgs& a, int B, hipStream_t s) {
 }
 }  // namespace
 
-int conv1d_tile_for(int Cout, int /*K*/) {
-  if (Cout > 64) return 0;
-  if (Cout > 32) return 1;
-  return 2;
+// Tile choice per conv shape, from the round-1 sweep on MI355X (profiles/r01_tune_conv.log,
+// HiFiGAN-v1 shapes at B=32 x 1034 frames).  `res`: the epilogue adds a residual.
+int conv1d_tile_for(int Cout, int K, int Cin, int dil, bool res) {
+  if ((K - 1) * dil > (K - 1) * DMAX) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
+  if (Cout > 64) {
+    if (Cin % 32 != 0) return K <= 3 ? 4 : 0;      // conv_pre (Cin 80), Glow start
+    if (K <= 3) return (res && Cout <= 128) ? 10 : 4;
+    return res ? 3 : 11;
+  }
+  if (Cout > 32) return (K <= 3 || res) ? 10 : 1;
+  return K >= 11 ? 2 : 8;
 }
 
 ConvTile conv1d_tile(int idx) {
-  TTS_REQUIRE(idx >= 0 && idx < 3, 3, "conv1d: bad tile index");
+  TTS_REQUIRE(idx >= 0 && idx < kNumConvTiles, 3, "conv1d: bad tile index");
   return kConvTiles[idx];
 }
+
+int conv1d_num_tiles() { return kNumConvTiles; }
 
 void launch_conv1d(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
   switch (K) {

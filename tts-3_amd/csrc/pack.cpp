@@ -9,11 +9,11 @@ namespace tts {
 // MFMA-fragment layout of the conv1d A operand (see conv1d_mfma_kernel):
 //   out[mb][c8][k][lane][j] = w[mb*32 + (lane&31)][c8*8 + 4*(lane>>5) + j][k]
 // mb over ceil(Cout/BM)*BM/32 blocks, c8 over n_chunks*CK/8 groups (zero padded), plus one
-// trailing fragment of slack for the kernel's one-step-ahead prefetch.
+// trailing fragments of slack for the kernel's prefetch (up to 2 steps ahead).
 int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t) {
   const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
   const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 8);
-  return mblocks * groups * K * 256 + 256;
+  return mblocks * groups * K * 256 + 512;
 }
 
 void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
@@ -29,7 +29,7 @@ void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, fl
             const int ci = c8 * 8 + 4 * (lane >> 5) + j;
             out[o++] = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
           }
-  for (int i = 0; i < 256; ++i) out[o++] = 0.f;
+  for (int i = 0; i < 512; ++i) out[o++] = 0.f;
 }
 
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t) {

@@ -117,6 +117,12 @@ SIGNATURES = {
     "tts_op_conv1d": (
         c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     ),
+    "tts_op_conv1d_bench": (
+        c_int,
+        [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+         POINTER(c_float), c_void_p],
+    ),
+    "tts_op_conv1d_num_tiles": (c_int, []),
     "tts_op_conv_transpose1d": (
         c_int,
         [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p],
