@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--comm", action="store_true",
                    help="also time an RCCL scatter of mels / gather of wavs from rank 0 (reported separately)")
+    p.add_argument("--math-mode", default="fp32", choices=["fp32", "fp32x6"],
+                   help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -111,7 +113,7 @@ def main():
     from tts_amd.vocoder import HifiganGenerator
 
     cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
-    g = HifiganGenerator(**cfg)
+    g = HifiganGenerator(**cfg, math_mode=a.math_mode)
     with contextlib.redirect_stdout(sys.stderr):  # the reference prints "Removing weight norm..."
         g.remove_weight_norm()
     g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False))
@@ -191,6 +193,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "math_mode": a.math_mode,
             "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
             "config": {
                 "workload": "HiFiGAN-v1 22.05kHz inference, [32,80,1024] mel per GPU (replicate pad 5), fp32",

@@ -44,6 +44,14 @@ extern "C" {
 #define TTS_ERR_UNSUPPORTED 3 /* configuration outside the implemented path                 */
 #define TTS_ERR_OOM 4         /* device allocation failed                                   */
 
+/* Arithmetic of the conv contractions (both produce fp32 results from fp32 inputs):
+ *   TTS_MATH_FP32     v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulation
+ *   TTS_MATH_FP32_X6  each fp32 operand split exactly into 3 bf16 pieces, the 6 significant
+ *                     cross products accumulated in fp32 on v_mfma_f32_32x32x16_bf16
+ *                     (dropped terms < 2^-26 relative; 2.67x the fp32-MFMA ceiling) */
+#define TTS_MATH_FP32 0
+#define TTS_MATH_FP32_X6 1
+
 #define TTS_MAX_UPSAMPLES 8
 #define TTS_MAX_KERNELS 4
 #define TTS_MAX_DILATIONS 4
@@ -79,6 +87,7 @@ typedef struct TtsHifiganCfg {
   int inference_padding;                /* default 5 (:173) */
   int cond_channels;                    /* 0 = no cond_layer (:227-228) */
   int conv_post_bias;                   /* default 1 (:177) */
+  int math_mode;                        /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
 } TtsHifiganCfg;
 
 /* Number of host weight tensors create() expects, and the element count of tensor idx.
@@ -140,6 +149,7 @@ typedef struct TtsGlowDecoderCfg {
   int num_squeeze;         /* 2 */
   int sigmoid_scale;       /* 0 */
   int c_in_channels;       /* 0 (speaker conditioning not implemented: must be 0) */
+  int math_mode;           /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
 } TtsGlowDecoderCfg;
 
 /* Host weight order, per flow block b < num_flow_blocks (flows 3b, 3b+1, 3b+2):
@@ -175,6 +185,7 @@ typedef struct TtsConv1dDesc {
   float in_slope, out_slope;
   int zmode;
   float zdiv;
+  int math_mode; /* TTS_MATH_FP32 / TTS_MATH_FP32_X6 */
 } TtsConv1dDesc;
 int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
                   const float* d_res, float* d_y, float* d_z, void* hip_stream);
@@ -184,8 +195,8 @@ int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, co
 int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
                         const float* d_res, float* d_y, float* d_z, int tile, int reps, float* ms,
                         void* hip_stream);
-/* Number of conv1d tile configurations compiled into the library. */
-int tts_op_conv1d_num_tiles(void);
+/* Number of conv1d tile configurations compiled into the library for a math mode. */
+int tts_op_conv1d_num_tiles(int math_mode);
 
 /* y = conv_transpose1d(act_in(x), w[Cin][Cout][K], b, stride, padding=(K-stride)/2);
  * requires K == 2*stride (every HiFiGAN config). */

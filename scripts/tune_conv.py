@@ -23,9 +23,13 @@ for C, L in ((256, 8 * TP), (128, 64 * TP), (64, 128 * TP), (32, 256 * TP)):
 
 
 def main():
-    only = sys.argv[1:] or None
+    args = sys.argv[1:]
+    mode = "fp32"
+    if args and args[0] in N.MATH_MODES:
+        mode, args = args[0], args[1:]
+    only = args or None
     dev = torch.device("cuda", 0)
-    ntiles = N.lib().tts_op_conv1d_num_tiles()
+    ntiles = N.lib().tts_op_conv1d_num_tiles(N.MATH_MODES[mode])
     reps = 5
     out = {}
     for name, Cin, Cout, T, K, dil, use_res in SHAPES:
@@ -37,7 +41,7 @@ def main():
         bias = (torch.randn(Cout, generator=g) * 0.1).numpy()
         res = torch.randn(B, Cout, T, generator=g).to(dev) if use_res else None
         flops = 2.0 * B * Cout * Cin * K * T
-        d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, 0, 0.1, 1.0 if use_res else 0.1, 0, 1.0)
+        d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, 0, 0.1, 1.0 if use_res else 0.1, 0, 1.0, N.MATH_MODES[mode])
         ref = None
         rows = []
         for tile in range(ntiles):
@@ -53,6 +57,12 @@ def main():
                 err = 0.0
             else:
                 err = (y - ref).abs().max().item()
+            if tile == 0 and mode != "fp32":  # compare the first tile against exact fp32
+                d32 = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, 0, 0.1, 1.0 if use_res else 0.1, 0, 1.0, 0)
+                y32 = torch.empty_like(y)
+                N.call("tts_op_conv1d", ctypes.byref(d32), N.ptr(x), N.ptr(w), N.ptr(bias), N.ptr(res), N.ptr(y32),
+                       None, N.stream_ptr(dev))
+                err = (y - y32).abs().max().item()
             rows.append((tile, ms.value, err))
         best = min((r for r in rows if r[1] is not None), key=lambda r: r[1])
         print(f"{name:18s} " + " ".join(
@@ -60,7 +70,7 @@ def main():
             for t, ms, e in rows) + f"  best t{best[0]} {flops / best[1] / 1e9:6.1f} TF", flush=True)
         out[name] = {"flops": flops, "tiles": {t: ms for t, ms, _ in rows}, "errors": {t: e for t, _, e in rows}}
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(REPO, "gpurun_out", "tune_conv.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(REPO, "gpurun_out", f"tune_conv_{mode}.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -15,19 +15,20 @@ GLOW_MAX_ABS = 1e-4
 GLOW_REL_RMS = 2e-5
 
 
-def build(cfg, seed, device):
+def build(cfg, seed, device, math_mode="fp32"):
     d = Decoder(cfg["in_channels"], cfg["hidden_channels"], cfg["kernel_size"], cfg["dilation_rate"],
                 cfg["num_flow_blocks"], cfg["num_coupling_layers"], dropout_p=0.05,
-                num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"])
+                num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"], math_mode=math_mode)
     d.load_state_dict(synthetic.glow_decoder_state_dict(**cfg, seed=seed))
     d.eval()
     d.store_inverse()
     return d.to(device)
 
 
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
 @pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
-def test_glow_reverse_vs_reference(cuda_device, name, meta, arr):
-    d = build(meta["config"], meta["seed"], cuda_device)
+def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
+    d = build(meta["config"], meta["seed"], cuda_device, mode)
     x = torch.from_numpy(arr["x"]).to(cuda_device)
     m = torch.from_numpy(arr["mask"]).to(cuda_device)
     y, logdet = d(x, m, reverse=True)

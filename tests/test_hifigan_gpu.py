@@ -50,8 +50,9 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
 @pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{i}" for i in range(len(CONV_CASES))])
-def test_op_conv1d(cuda_device, case):
+def test_op_conv1d(cuda_device, case, mode):
     B, Cin, Cout, T, K, dil, rep, s_in, s_out, use_res, zmode = case
     g = _rng(hash(case) & 0xFFFF)
     x = torch.randn(B, Cin, T, generator=g)
@@ -67,7 +68,7 @@ def test_op_conv1d(cuda_device, case):
     if res is not None:
         v = v + res.double()
     ref = {0: v, 1: v, 2: z0.double() + v, 3: (z0.double() + v) / 3.0}[zmode]
-    d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, rep, s_in, s_out, zmode, 3.0)
+    d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, rep, s_in, s_out, zmode, 3.0, N.MATH_MODES[mode])
     xd = x.to(cuda_device)
     resd = res.to(cuda_device) if res is not None else None
     y = torch.full((B, Cout, To), float("nan"), device=cuda_device)
@@ -127,8 +128,8 @@ def test_op_conv_post(cuda_device, B, Cin, T):
 HIFI = goldens("hifigan")
 
 
-def build(cfg, seed, device):
-    g = HifiganGenerator(**hifigan_ctor(cfg))
+def build(cfg, seed, device, math_mode="fp32"):
+    g = HifiganGenerator(**hifigan_ctor(cfg), math_mode=math_mode)
     g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=seed, weight_norm=True))
     g.eval()
     if cfg.get("conv_pre_weight_norm", True):
@@ -136,10 +137,11 @@ def build(cfg, seed, device):
     return g.to(device)
 
 
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
 @pytest.mark.parametrize("name,meta,arr", HIFI, ids=[h[0] for h in HIFI])
-def test_generator_vs_reference_goldens(cuda_device, name, meta, arr):
+def test_generator_vs_reference_goldens(cuda_device, name, meta, arr, mode):
     cfg = meta["config"]
-    g = build(cfg, meta["seed"], cuda_device)
+    g = build(cfg, meta["seed"], cuda_device, mode)
     mel = torch.from_numpy(arr["mel"]).to(cuda_device)
     gv = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
     out = g.inference(mel, gv) if gv is not None else g.inference(mel)
@@ -201,10 +203,11 @@ def test_profiled_forward_records(cuda_device):
 
 
 @pytest.mark.slow
-def test_benchmark_size_properties(cuda_device):
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+def test_benchmark_size_properties(cuda_device, mode):
     """Config 2 of BASELINE.json: B=32 x 1024 frames, HiFiGAN-v1, fp32."""
     sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
-    g = HifiganGenerator(**V1)
+    g = HifiganGenerator(**V1, math_mode=mode)
     g.remove_weight_norm()
     g.load_state_dict(sd)
     g = g.to(cuda_device)
@@ -220,3 +223,17 @@ def test_benchmark_size_properties(cuda_device):
         assert torch.equal(single[0], out[i]), f"batch invariance, item {i}"
     ref = hifigan_ref.hifigan_forward(sd, mel[17:18].cpu(), pad=5, dtype=torch.float64, **V1)
     assert_close_fp32(out[17:18].cpu(), ref, "B=32 item 17 vs fp64 oracle")
+
+
+def test_x6_accuracy_not_worse_than_fp32(cuda_device):
+    """The bf16x6 split is fp32-faithful: its error vs the fp64 reference matches exact-fp32 MFMA."""
+    name, meta, arr = [h for h in HIFI if h[0] == "hifigan_v1_b2_t32"][0]
+    errs = {}
+    for mode in ("fp32", "fp32x6"):
+        g = build(meta["config"], meta["seed"], cuda_device, mode)
+        out = g.inference(torch.from_numpy(arr["mel"]).to(cuda_device)).cpu().numpy()
+        errs[mode] = (max_abs(out, arr["out_ref_fp64"]), rel_rms(out, arr["out_ref_fp64"]))
+    ref32 = (max_abs(arr["out_ref_fp32"], arr["out_ref_fp64"]), rel_rms(arr["out_ref_fp32"], arr["out_ref_fp64"]))
+    print("max|d|, rel-RMS vs fp64:", errs, "reference fp32 CPU:", ref32)
+    assert errs["fp32x6"][1] <= 2.0 * max(errs["fp32"][1], ref32[1])
+    assert errs["fp32x6"][0] <= 2.0 * max(errs["fp32"][0], ref32[0])

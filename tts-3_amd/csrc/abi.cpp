@@ -52,7 +52,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 100; }
+int tts_abi_version(void) { return 101; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -201,10 +201,12 @@ static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float
   TTS_REQUIRE((d->K % 2) == 1, 3, "conv1d: only odd kernel sizes ('same' padding)");
   TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
   TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
-  if (tile < 0) tile = tts::conv1d_tile_for(d->Cout, d->K, d->Cin, d->dil, d_res != nullptr);
-  const tts::ConvTile t = tts::conv1d_tile(tile);
-  std::vector<float> packed(tts::packed_conv1d_numel(d->Cout, d->Cin, d->K, t));
-  tts::pack_conv1d(h_w, d->Cout, d->Cin, d->K, t, packed.data());
+  const int mode = d->math_mode;
+  TTS_REQUIRE(mode == tts::MATH_FP32 || mode == tts::MATH_FP32_X6, 1, "unknown math_mode");
+  if (tile < 0) tile = tts::conv_tile_for(mode, d->Cout, d->K, d->Cin, d->dil, d_res != nullptr);
+  const tts::ConvTile t = tts::conv_tile(mode, tile);
+  std::vector<float> packed(tts::packed_conv_numel(mode, d->Cout, d->Cin, d->K, t));
+  tts::pack_conv(mode, h_w, d->Cout, d->Cin, d->K, t, packed.data());
   std::vector<float> bias((size_t)tts::ceil_div(d->Cout, t.BM) * t.BM, 0.f);
   std::memcpy(bias.data(), h_b, sizeof(float) * d->Cout);
   TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
@@ -216,14 +218,14 @@ static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float
   a.in_slope = d->in_slope; a.out_slope = d->out_slope; a.zmode = d->zmode; a.zdiv = d->zdiv;
   auto s = static_cast<hipStream_t>(hip_stream);
   if (reps <= 0) {
-    tts::launch_conv1d(a, d->B, d->K, tile, s);
+    tts::launch_conv(mode, a, d->B, d->K, tile, s);
   } else {
-    tts::launch_conv1d(a, d->B, d->K, tile, s);  // warm-up
+    tts::launch_conv(mode, a, d->B, d->K, tile, s);  // warm-up
     hipEvent_t e0, e1;
     TTS_HIP_CHECK(hipEventCreate(&e0));
     TTS_HIP_CHECK(hipEventCreate(&e1));
     TTS_HIP_CHECK(hipEventRecord(e0, s));
-    for (int r = 0; r < reps; ++r) tts::launch_conv1d(a, d->B, d->K, tile, s);
+    for (int r = 0; r < reps; ++r) tts::launch_conv(mode, a, d->B, d->K, tile, s);
     TTS_HIP_CHECK(hipEventRecord(e1, s));
     TTS_HIP_CHECK(hipEventSynchronize(e1));
     float total = 0.f;
@@ -246,7 +248,9 @@ int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h
   return guarded([&] { op_conv1d_impl(d, d_x, h_w, h_b, d_res, d_y, d_z, tile, reps, ms, hip_stream); });
 }
 
-int tts_op_conv1d_num_tiles(void) { return tts::conv1d_num_tiles(); }
+int tts_op_conv1d_num_tiles(int math_mode) {
+  return math_mode == tts::MATH_FP32_X6 ? tts::conv1d_x6_num_tiles() : tts::conv1d_num_tiles();
+}
 
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
                             const float* h_b, int Cout, int K, int stride, float in_slope,

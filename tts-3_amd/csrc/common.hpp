@@ -96,6 +96,26 @@ void launch_conv_post(const PostArgs& a, int B, hipStream_t s);
 void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
                      int C0, hipStream_t s);
 
+// bf16x6 split-precision conv1d (kernels_conv_x6.hip)
+ConvTile conv1d_x6_tile(int idx);
+int conv1d_x6_num_tiles();
+int conv1d_x6_tile_for(int Cout, int K, int Cin, int dil, bool res);
+void launch_conv1d_x6(const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
+
+// Math modes (TTS_MATH_* in tts_mi355x.h)
+constexpr int MATH_FP32 = 0;     // v_mfma_f32_32x32x2_f32
+constexpr int MATH_FP32_X6 = 1;  // bf16x6 split on v_mfma_f32_32x32x16_bf16
+
+// Mode-dispatching helpers used by the executors and the op entry points.
+inline ConvTile conv_tile(int mode, int idx) { return mode == MATH_FP32_X6 ? conv1d_x6_tile(idx) : conv1d_tile(idx); }
+inline int conv_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
+  return mode == MATH_FP32_X6 ? conv1d_x6_tile_for(Cout, K, Cin, dil, res) : conv1d_tile_for(Cout, K, Cin, dil, res);
+}
+inline void launch_conv(int mode, const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  if (mode == MATH_FP32_X6) launch_conv1d_x6(a, B, K, tile, s);
+  else launch_conv1d(a, B, K, tile, s);
+}
+
 // Host-side weight packing (pack.cpp).
 // Conv1d torch weight [Cout][Cin][K] -> MFMA fragments [mblock32][cgroup8][K][64][4] (+slack).
 void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
@@ -103,6 +123,15 @@ int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] -> [Cout_pad/BM][n_chunks][2U][CK][BM].
 void pack_convT(const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out);
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t);
+void pack_conv1d_x6(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
+int64_t packed_conv1d_x6_numel(int Cout, int Cin, int K, const ConvTile& t);
+inline int64_t packed_conv_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
+  return mode == MATH_FP32_X6 ? packed_conv1d_x6_numel(Cout, Cin, K, t) : packed_conv1d_numel(Cout, Cin, K, t);
+}
+inline void pack_conv(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
+  if (mode == MATH_FP32_X6) pack_conv1d_x6(w, Cout, Cin, K, t, out);
+  else pack_conv1d(w, Cout, Cin, K, t, out);
+}
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 

@@ -50,6 +50,7 @@ void glow_validate(const TtsGlowDecoderCfg& c) {
     d *= c.dilation_rate;
   }
   TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned Glow decoder (c_in_channels > 0) not implemented");
+  TTS_REQUIRE(c.math_mode == MATH_FP32 || c.math_mode == MATH_FP32_X6, 1, "unknown math_mode");
 }
 
 GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, int device)
@@ -76,13 +77,14 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   };
   auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
     cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
-    cv.tile = conv1d_tile_for(Cout, K, Cin, dil, false);
-    const ConvTile t = conv1d_tile(cv.tile);
+    const int mode = cfg_.math_mode;
+    cv.tile = conv_tile_for(mode, Cout, K, Cin, dil, false);
+    const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
-    const size_t n = packed_conv1d_numel(Cout, Cin, K, t);
+    const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);
     const size_t off = host.size();
     host.resize(off + align(n), 0.f);
-    pack_conv1d(w, Cout, Cin, K, t, host.data() + off);
+    pack_conv(mode, w, Cout, Cin, K, t, host.data() + off);
     fix.push_back({off, &cv.w});
     const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
     const size_t offb = host.size();
@@ -169,7 +171,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th;
     a.dil = cv.dil; a.pad = cv.dil * (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;
     a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = 0; a.zdiv = 1.f;
-    launch_conv1d(a, B, cv.K, cv.tile, s);
+    launch_conv(cfg_.math_mode, a, B, cv.K, cv.tile, s);
   };
 
   // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1

@@ -77,6 +77,7 @@ void hifigan_validate(const TtsHifiganCfg& c) {
   }
   TTS_REQUIRE(c.inference_padding >= 0, 1, "inference_padding must be >= 0");
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
+  TTS_REQUIRE(c.math_mode == MATH_FP32 || c.math_mode == MATH_FP32_X6, 1, "unknown math_mode");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -90,15 +91,16 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
 
   // 1) describe layers, 2) size the arena, 3) pack on host, 4) one upload.
   const int C0 = cfg_.upsample_initial_channel;
+  const int mode = cfg_.math_mode;
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res) {
     ConvLayer L;
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
-    L.tile = conv1d_tile_for(Cout, K, Cin, dil, res);
-    const ConvTile t = conv1d_tile(L.tile);
+    L.tile = conv_tile_for(mode, Cout, K, Cin, dil, res);
+    const ConvTile t = conv_tile(mode, L.tile);
     L.n_chunks = ceil_div(Cin, t.CK);
-    L.w_numel = packed_conv1d_numel(Cout, Cin, K, t);
+    L.w_numel = packed_conv_numel(mode, Cout, Cin, K, t);
     L.b_numel = (int64_t)ceil_div(Cout, t.BM) * t.BM;
     L.name = std::string(fam) + "_k" + std::to_string(K) + "_c" + std::to_string(Cout);
     return L;
@@ -172,8 +174,8 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     // src[0] is conv_pre; src[1..] resblocks
     size_t si = 0;
     for (auto* c : convs) {
-      const ConvTile t = conv1d_tile(c->tile);
-      pack_conv1d(src[si].first, c->Cout, c->Cin, c->K, t, host.data() + off);
+      const ConvTile t = conv_tile(mode, c->tile);
+      pack_conv(mode, src[si].first, c->Cout, c->Cin, c->K, t, host.data() + off);
       offs.push_back(off); off += align(c->w_numel);
       std::memcpy(host.data() + off, src[si].second, sizeof(float) * c->Cout);
       offs.push_back(off); off += align(c->b_numel);
@@ -282,7 +284,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     double bytes = 4.0 * ((double)B * Ld.Cin * Tin + (double)Ld.Cout * Ld.Cin * Ld.K + (double)B * Ld.Cout * Tout);
     if (res) bytes += 4.0 * B * Ld.Cout * (double)Tout;
     if (zmode >= 2) bytes += 4.0 * B * Ld.Cout * (double)Tout;
-    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv1d(a, B, Ld.K, Ld.tile, s); });
+    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv(cfg_.math_mode, a, B, Ld.K, Ld.tile, s); });
   };
 
   // conv_pre on the replicate-padded mel (hifigan_generator.py:281, :249) [+ cond_layer(g), :250-251]

@@ -17,7 +17,7 @@
 // [CK][BN + (K-1)*dil] are staged in LDS once and reused by every tap and every wave.
 // Double-buffered: the next chunk is fetched to registers while the MFMAs run on the
 // current one; one barrier per chunk.
-#include "common.hpp"
+#include "conv_device.hpp"
 
 namespace tts {
 
@@ -47,14 +47,6 @@ struct ConvCfg {
   static_assert(WM * WN == 4, "4 waves per workgroup");
   static_assert(PD == 1 || PD == 2, "A prefetch distance");
 };
-
-// LDS float offset of channel quad q (0/1) of input row r in group g.  The quad index is
-// XOR-swizzled with bit 3 of the row: every ds_read_b128 lane group (16 lanes, rows
-// r0 + {0-3,12-15,20-27} or {4-11,16-19,28-31}) then hits 16 distinct 16-byte bank slots
-// for ANY row shift r0 (the tap offset k*dil), with no padding.
-__device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
-  return (g * xrows + r) * 8 + 4 * (q ^ ((r >> 3) & 1));
-}
 
 template <int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
 __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
@@ -209,40 +201,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
     __syncthreads();
   }
 
-  // Epilogue.  32x32 accumulator: lane holds column l32, rows (r&3) + 8*(r>>2) + 4*half.
-  const int Cout = a.Cout;
-  const float oslope = a.out_slope;
-  const int zmode = a.zmode;
-  const float zdiv = a.zdiv;
-  const float* __restrict__ res = a.res;
-#pragma unroll
-  for (int m = 0; m < TM; ++m) {
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      const int t = t0 + wn * TN * 32 + n * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = mt * BM + wm * TM * 32 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (co < Cout && t < Tout) {
-          const size_t idx = ((size_t)b * Cout + co) * Tout + t;
-          float v = acc[m][n][r] + a.bias[co];
-          if (a.cvec) v += a.cvec[(size_t)b * Cout + co];
-          if (a.mask) v *= a.mask[(size_t)b * Tout + t];
-          v = lrelu(v, oslope);
-          if (res) v += res[idx];
-          if (zmode == 0) {
-            a.y[idx] = v;
-          } else if (zmode == 1) {
-            a.z[idx] = v;
-          } else if (zmode == 2) {
-            a.z[idx] = a.z[idx] + v;
-          } else {
-            a.z[idx] = (a.z[idx] + v) / zdiv;
-          }
-        }
-      }
-    }
-  }
+  conv_epilogue<TM, TN>(a, acc, b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
 }
 
 // ---------------------------------------------------------------------------------------

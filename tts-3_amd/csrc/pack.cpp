@@ -32,6 +32,60 @@ void pack_conv1d(const float* w, int Cout, int Cin, int K, const ConvTile& t, fl
   for (int i = 0; i < 512; ++i) out[o++] = 0.f;
 }
 
+// bf16x6 split of an fp32 value: x = p0 + p1 + p2 exactly, round-to-nearest-even per piece
+// (same rounding as the device's v_cvt_pk_bf16_f32).
+static inline uint16_t f2bf_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static inline float bf2f(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+void split3_host(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+  p0 = f2bf_rne(x);
+  const float r1 = x - bf2f(p0);
+  p1 = f2bf_rne(r1);
+  const float r2 = r1 - bf2f(p1);
+  p2 = f2bf_rne(r2);
+}
+
+// bf16x6 A-operand fragments (conv1d_x6_kernel), in floats (2 bf16 per float):
+//   out[mb][c16][k][piece][lane][j] = piece_p(w[mb*32 + (lane&31)][c16*16 + 8*(lane>>5) + j][k])
+// plus 2 steps of slack for the prefetch.
+int64_t packed_conv1d_x6_numel(int Cout, int Cin, int K, const ConvTile& t) {
+  const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
+  const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 16);
+  return (mblocks * groups * K + 2) * 3 * 64 * 4;
+}
+
+void pack_conv1d_x6(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f) {
+  uint16_t* out = reinterpret_cast<uint16_t*>(out_f);
+  const int mblocks = ceil_div(Cout, t.BM) * (t.BM / 32);
+  const int groups = ceil_div(Cin, t.CK) * (t.CK / 16);
+  int64_t o = 0;
+  for (int mb = 0; mb < mblocks; ++mb)
+    for (int c16 = 0; c16 < groups; ++c16)
+      for (int k = 0; k < K; ++k) {
+        uint16_t pc[3][64][8];
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int co = mb * 32 + (lane & 31);
+            const int ci = c16 * 16 + 8 * (lane >> 5) + j;
+            const float v = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
+            split3_host(v, pc[0][lane][j], pc[1][lane][j], pc[2][lane][j]);
+          }
+        for (int p = 0; p < 3; ++p)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) out[o++] = pc[p][lane][j];
+      }
+  for (int i = 0; i < 2 * 3 * 64 * 8; ++i) out[o++] = 0;
+}
+
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t) {
   const int64_t mtiles = ceil_div(Cout, t.BM);
   const int64_t chunks = ceil_div(Cin, t.CK);

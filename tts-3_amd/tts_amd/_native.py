@@ -25,6 +25,9 @@ TTS_ERR_HIP = 2
 TTS_ERR_UNSUPPORTED = 3
 TTS_ERR_OOM = 4
 
+# math modes (TTS_MATH_* in tts_mi355x.h)
+MATH_MODES = {"fp32": 0, "fp32x6": 1}
+
 MAX_UPSAMPLES = 8
 MAX_KERNELS = 4
 MAX_DILATIONS = 4
@@ -46,6 +49,7 @@ class TtsHifiganCfg(Structure):
         ("inference_padding", c_int),
         ("cond_channels", c_int),
         ("conv_post_bias", c_int),
+        ("math_mode", c_int),
     ]
 
 
@@ -61,6 +65,7 @@ class TtsGlowDecoderCfg(Structure):
         ("num_squeeze", c_int),
         ("sigmoid_scale", c_int),
         ("c_in_channels", c_int),
+        ("math_mode", c_int),
     ]
 
 
@@ -81,6 +86,7 @@ class TtsConv1dDesc(Structure):
         ("out_slope", c_float),
         ("zmode", c_int),
         ("zdiv", c_float),
+        ("math_mode", c_int),
     ]
 
 
@@ -122,7 +128,7 @@ SIGNATURES = {
         [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
          POINTER(c_float), c_void_p],
     ),
-    "tts_op_conv1d_num_tiles": (c_int, []),
+    "tts_op_conv1d_num_tiles": (c_int, [c_int]),
     "tts_op_conv_transpose1d": (
         c_int,
         [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p],

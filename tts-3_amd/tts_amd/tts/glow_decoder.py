@@ -135,8 +135,11 @@ def _t(t: torch.Tensor) -> np.ndarray:
 class Decoder(nn.Module):
     def __init__(self, in_channels, hidden_channels, kernel_size, dilation_rate, num_flow_blocks,
                  num_coupling_layers, dropout_p=0.0, num_splits=4, num_squeeze=2, sigmoid_scale=False,
-                 c_in_channels=0):
+                 c_in_channels=0, math_mode: str = "fp32"):
         super().__init__()
+        if math_mode not in N.MATH_MODES:
+            raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
+        self.math_mode = math_mode
         self.in_channels = in_channels
         self.hidden_channels = hidden_channels
         self.kernel_size = kernel_size
@@ -167,6 +170,7 @@ class Decoder(nn.Module):
         c.num_squeeze = num_squeeze
         c.sigmoid_scale = 1 if sigmoid_scale else 0
         c.c_in_channels = c_in_channels
+        c.math_mode = N.MATH_MODES[math_mode]
         self._cfg = c
         self._handle = None
         self._handle_key = None

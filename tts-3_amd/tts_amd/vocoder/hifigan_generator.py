@@ -109,8 +109,16 @@ class HifiganGenerator(nn.Module):
         conv_pre_weight_norm: bool = True,
         conv_post_weight_norm: bool = True,
         conv_post_bias: bool = True,
+        math_mode: str = "fp32",
     ):
+        """Arguments as the reference (:163-178).  ``math_mode`` selects how the conv contractions
+        run on MI355X: ``"fp32"`` (v_mfma_f32_32x32x2_f32) or ``"fp32x6"`` (fp32 operands split
+        exactly into 3 bf16 pieces, 6 cross products accumulated in fp32 on the bf16 matrix
+        cores; fp32-faithful, see include/tts_mi355x.h)."""
         super().__init__()
+        if math_mode not in N.MATH_MODES:
+            raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
+        self.math_mode = math_mode
         self.inference_padding = inference_padding
         self.num_kernels = len(resblock_kernel_sizes)
         self.num_upsamples = len(upsample_factors)
@@ -138,6 +146,7 @@ class HifiganGenerator(nn.Module):
         c.inference_padding = inference_padding
         c.cond_channels = cond_channels
         c.conv_post_bias = 1 if conv_post_bias else 0
+        c.math_mode = N.MATH_MODES[math_mode]
         self.hop_length = int(np.prod(upsample_factors))
 
         # parameter tree identical to the reference (:203-234)
