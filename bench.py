@@ -28,6 +28,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
+# ceiling of each math mode in algorithmic fp32 FLOP/s: fp32x6 issues 6 bf16 MFMA products
+# per fp32 multiply-accumulate (include/tts_mi355x.h TTS_MATH_FP32_X6)
+MODE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS / 6.0}
 HBM_PEAK_GBS = 8000.0
 SAMPLE_RATE = 22050
 METRIC = "audio samples/sec + RTF, HiFiGAN-v1 22.05kHz 80-mel, batch 32 @ 1/2/4/8 GPU"
@@ -44,8 +48,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--comm", action="store_true",
                    help="also time an RCCL scatter of mels / gather of wavs from rank 0 (reported separately)")
-    p.add_argument("--math-mode", default="fp32", choices=["fp32", "fp32x6"],
+    p.add_argument("--math-mode", default="fp32x6", choices=["fp32", "fp32x6"],
                    help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
+    p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -98,6 +103,60 @@ def cpu_baseline(budget_s: float):
     }
 
 
+def build_generator(math_mode, dev):
+    from tts_amd import synthetic
+    from tts_amd.config import HIFIGAN_V1
+    from tts_amd.vocoder import HifiganGenerator
+
+    cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+    g = HifiganGenerator(**cfg, math_mode=math_mode)
+    with contextlib.redirect_stdout(sys.stderr):  # the reference prints "Removing weight norm..."
+        g.remove_weight_norm()
+    g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False))
+    g.eval()
+    return g.to(dev)
+
+
+def time_steps(g, mel, steps, warmup, dev, world):
+    for _ in range(warmup):
+        g.inference(mel)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.inference(mel)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()) / steps * 1e3
+
+
+def accuracy_check(gens, dev):
+    """Each math mode vs the fp64 CPU oracle on a small sample (B=1 x 48 frames)."""
+    sys.path.insert(0, REPO)
+    from oracle import hifigan_ref  # test infrastructure: the checker, not the measured path
+    from tts_amd import synthetic
+    from tts_amd.config import HIFIGAN_V1
+
+    cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
+    sd = synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False)
+    mel = synthetic.mel(1, 48, seed=7)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **cfg)
+    out = {}
+    for mode, g in gens.items():
+        y = g.inference(mel.to(dev)).cpu().double()
+        d = y - ref
+        out[mode] = {"max_abs": float(d.abs().max()), "rel_rms": float(d.pow(2).mean().sqrt() / ref.pow(2).mean().sqrt())}
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,40 +168,13 @@ def main():
     dev = torch.device("cuda", local)
 
     from tts_amd import synthetic
-    from tts_amd.config import HIFIGAN_V1
-    from tts_amd.vocoder import HifiganGenerator
 
-    cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
-    g = HifiganGenerator(**cfg, math_mode=a.math_mode)
-    with contextlib.redirect_stdout(sys.stderr):  # the reference prints "Removing weight norm..."
-        g.remove_weight_norm()
-    g.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False))
-    g.eval()
-    g = g.to(dev)
+    g = build_generator(a.math_mode, dev)
     B, T, pad = a.batch, a.frames, g.inference_padding
     mel = synthetic.mel(B, T, seed=rank).to(dev)
     g.reserve(B, T)
     torch.cuda.synchronize(dev)
-
-    for _ in range(a.warmup):
-        g.inference(mel)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        out = g.inference(mel)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    ms_per_step = el / a.steps * 1e3
+    ms_per_step = time_steps(g, mel, a.steps, a.warmup, dev, world)
     samples_per_step = B * g.hop_length * (T + 2 * pad)  # per GPU
     value = world * samples_per_step / (ms_per_step / 1e3)
     rtf = (ms_per_step / 1e3) / (world * samples_per_step / SAMPLE_RATE)
@@ -157,7 +189,7 @@ def main():
         torch.cuda.synchronize(dev)
         c0 = time.perf_counter()
         shard = scatter_batch(full, n, (80, T), dev)
-        wav = gather_batch(g.inference(shard), n)
+        gather_batch(g.inference(shard), n)
         torch.cuda.synchronize(dev)
         comm = {"scatter_infer_gather_ms": (time.perf_counter() - c0) * 1e3, "utterances": n}
 
@@ -172,12 +204,24 @@ def main():
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            traffic = tj.get("per_launch_bytes", {}).get(fam_name)
+            traffic = tj.get("per_launch_bytes", {}).get(f"{a.math_mode}:{fam_name}")
         except Exception:
             traffic = None
 
+    alt = None
+    gens = {a.math_mode: g}
+    if not a.no_alt:
+        other = "fp32" if a.math_mode == "fp32x6" else "fp32x6"
+        g2 = build_generator(other, dev)
+        g2.reserve(B, T)
+        ms2 = time_steps(g2, mel, max(3, a.steps // 2), 1, dev, world)
+        alt = {"math_mode": other, "ms_per_step": ms2, "value": world * samples_per_step / (ms2 / 1e3)}
+        gens[other] = g2
+
     cpu = None
+    acc = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        acc = accuracy_check(gens, dev)
         cpu = cpu_baseline(a.cpu_seconds)
 
     if rank == 0:
@@ -192,7 +236,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if a.math_mode == "fp32" else "fp32 (bf16x6 split on bf16 MFMA, fp32 accumulate)",
             "math_mode": a.math_mode,
             "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
             "config": {
@@ -210,15 +254,18 @@ def main():
                 "kernel": fam_name,
                 "launches_per_step": fam["n"],
                 "achieved": achieved,
-                "peak": FP32_PEAK_TFLOPS,
+                "peak": MODE_PEAK[a.math_mode],
+                "peak_basis": "fp32 MFMA 157.3 TF" if a.math_mode == "fp32" else "bf16 dense MFMA 2.5 PF / 6 products per fp32 MAC",
                 "unit": "TFLOP/s",
-                "frac": achieved / FP32_PEAK_TFLOPS,
+                "frac": achieved / MODE_PEAK[a.math_mode],
                 "traffic": traffic,
                 "flops_per_launch": per_launch_flops,
                 "avg_launch_ms": avg_ms,
             },
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
             "cpu_baseline": cpu,
+            "alt_math_mode": alt,
+            "accuracy_vs_fp64_oracle": acc,
         }
         if comm:
             rec["comm"] = comm
