@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--math-mode", default="fp32x6", choices=["fp32", "fp32x6"],
                    help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
     p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
+    p.add_argument("--no-glow", action="store_true", help="skip the Glow-TTS decoder measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -157,6 +158,67 @@ def accuracy_check(gens, dev):
     return out
 
 
+def glow_bench(dev, math_mode, steps=10, warmup=3, B=16, T=768, cpu=True):
+    """Glow-TTS decoder reverse flow (config 3's decoder: B=16, T=768 mel frames, LJSpeech cfg)."""
+    from tts_amd import synthetic
+    from tts_amd.config import GLOW_TTS_DECODER as G
+    from tts_amd.tts import Decoder
+
+    cfg = dict(in_channels=G["in_channels"], hidden_channels=G["hidden_channels"], kernel_size=G["kernel_size"],
+               dilation_rate=G["dilation_rate"], num_flow_blocks=G["num_flow_blocks"],
+               num_coupling_layers=G["num_coupling_layers"], num_splits=G["num_splits"],
+               num_squeeze=G["num_squeeze"])
+    sd = synthetic.glow_decoder_state_dict(**cfg, seed=4321)
+    d = Decoder(**cfg, dropout_p=G["dropout_p"], math_mode=math_mode)
+    d.load_state_dict(sd)
+    d.eval()
+    d.store_inverse()
+    d = d.to(dev)
+    x = torch.randn(B, cfg["in_channels"], T, generator=torch.Generator().manual_seed(3)).to(dev)
+    m = torch.ones(B, 1, T, device=dev)
+    for _ in range(warmup):
+        d(x, m, reverse=True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        d(x, m, reverse=True)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    _, rows = d.profile(x, m)
+    name, fam, fams = dominant_kernel(rows)
+    flops = sum(r["flops"] for r in rows)
+    out = {
+        "workload": f"Glow-TTS decoder reverse, [{B},80,{T}] (12 flows x 4 WN layers, hidden 192, k5)",
+        "math_mode": math_mode,
+        "ms_per_step": ms,
+        "mel_frames_per_s": B * T / (ms / 1e3),
+        "launches_per_step": len(rows),
+        "tflops": flops / (ms / 1e3) / 1e12,
+        "kernel_sum_ms": sum(r["ms"] for r in rows),
+        "dominant_kernel": {"name": name, "avg_launch_ms": fam["ms"] / fam["n"],
+                            "achieved_tflops": fam["flops"] / fam["ms"] / 1e9, "launches": fam["n"]},
+        "breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
+    }
+    if cpu:
+        sys.path.insert(0, REPO)
+        from oracle import glow_ref  # test infrastructure: the baseline being timed, not the product
+
+        xs = x[:2].cpu()
+        ms_ = m[:2].cpu()
+        glow_ref.glow_decoder_reverse(sd, xs[:, :, :64], ms_[:, :, :64], dtype=torch.float32, **cfg)
+        n, c0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while True:
+                glow_ref.glow_decoder_reverse(sd, xs, ms_, dtype=torch.float32, **cfg)
+                n += 1
+                if time.perf_counter() - c0 > 5.0:
+                    break
+        el = time.perf_counter() - c0
+        out["cpu_baseline"] = {"mel_frames_per_s": n * 2 * T / el, "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"{n} x Decoder.forward(reverse=True) on [2,80,{T}] (oracle/glow_ref.py fp32)"}
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -224,6 +286,10 @@ def main():
         acc = accuracy_check(gens, dev)
         cpu = cpu_baseline(a.cpu_seconds)
 
+    glow = None
+    if rank == 0 and not a.no_glow:
+        glow = glow_bench(dev, a.math_mode, cpu=(world == 1 and not a.no_cpu_baseline))
+
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -265,6 +331,7 @@ def main():
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
             "cpu_baseline": cpu,
             "alt_math_mode": alt,
+            "glow_decoder": glow,
             "accuracy_vs_fp64_oracle": acc,
         }
         if comm:

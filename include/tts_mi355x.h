@@ -169,6 +169,10 @@ int tts_glow_decoder_destroy(void* handle);
  * implemented (the inference direction, glow_tts.py:363). */
 int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, int B, int C,
                              int T, int reverse, float* d_y, void* hip_stream);
+/* Same with a hipEvent pair around every launch (synchronises; see tts_hifigan_forward_profiled). */
+int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, int B, int C,
+                                      int T, int reverse, float* d_y, void* hip_stream,
+                                      TtsLaunchRecord* records, int max_records, int* n_records);
 
 /* ------------------------------------------------------------------------------------ */
 /* Single-op entry points (test / tuning surface).  These pack the host weights into a     */

@@ -35,6 +35,20 @@ int guarded(F&& f) {
   }
 }
 
+void export_records(const tts::Profiler& prof, TtsLaunchRecord* records, int max_records, int* n_records) {
+  *n_records = (int)prof.recs.size();
+  for (int i = 0; i < (int)prof.recs.size() && i < max_records && records; ++i) {
+    const auto& r = prof.recs[i];
+    std::memset(records[i].name, 0, sizeof(records[i].name));
+    std::strncpy(records[i].name, r.name.c_str(), sizeof(records[i].name) - 1);
+    records[i].flops = r.flops;
+    records[i].bytes = r.bytes;
+    float ms = 0.f;
+    TTS_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+    records[i].ms = ms;
+  }
+}
+
 // RAII device buffer for the single-op entry points.
 struct TmpDev {
   float* p = nullptr;
@@ -131,17 +145,7 @@ int tts_hifigan_forward_profiled(void* handle, const float* d_mel, int B, int C,
       h->forward(d_mel, B, C, T, pad, d_g, d_wav, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
-    *n_records = (int)prof.recs.size();
-    for (int i = 0; i < (int)prof.recs.size() && i < max_records && records; ++i) {
-      auto& r = prof.recs[i];
-      std::memset(records[i].name, 0, sizeof(records[i].name));
-      std::strncpy(records[i].name, r.name.c_str(), sizeof(records[i].name) - 1);
-      records[i].flops = r.flops;
-      records[i].bytes = r.bytes;
-      float ms = 0.f;
-      TTS_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
-      records[i].ms = ms;
-    }
+    export_records(prof, records, max_records, n_records);
   });
 }
 
@@ -188,6 +192,24 @@ int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask
     TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
     static_cast<tts::GlowDecoder*>(handle)->reverse(d_x, d_mask, B, C, T, d_y,
                                                     static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, int B, int C,
+                                      int T, int reverse, float* d_y, void* hip_stream,
+                                      TtsLaunchRecord* records, int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    auto* h = static_cast<tts::GlowDecoder*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->reverse(d_x, d_mask, B, C, T, d_y, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
   });
 }
 

@@ -133,7 +133,8 @@ void GlowDecoder::reserve(int B, int Th) {
   ws_bytes_ = need;
 }
 
-void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s) {
+void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s,
+                          Profiler* prof) {
   TTS_REQUIRE(x && mask && y, 1, "NULL input/output pointer");
   TTS_REQUIRE(B >= 1, 1, "batch must be >= 1");
   TTS_REQUIRE(C == cfg_.in_channels, 1, "channel count does not match the decoder");
@@ -158,41 +159,46 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   float* msq = p;
 
   // squeeze (decoder.py:128, :8-28); without squeeze the mask is used as is
+  const double P = (double)B * Th;  // squeezed positions
   if (nsq > 1) {
-    launch_glow_squeeze(x, mask, xs, msq, B, C, T, nsq, s);
+    run(prof, s, "glow_squeeze", 0.0, 8.0 * P * C2 + 8.0 * P,
+        [&] { launch_glow_squeeze(x, mask, xs, msq, B, C, T, nsq, s); });
   } else {
     TTS_HIP_CHECK(hipMemcpyAsync(xs, x, plane * C2 * sizeof(float), hipMemcpyDeviceToDevice, s));
     TTS_HIP_CHECK(hipMemcpyAsync(msq, mask, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
 
-  auto conv = [&](const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m) {
+  auto conv = [&](const char* name, const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m) {
     Conv1dArgs a{};
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride;
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th;
     a.dil = cv.dil; a.pad = cv.dil * (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;
     a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = 0; a.zdiv = 1.f;
-    launch_conv(cfg_.math_mode, a, B, cv.K, cv.tile, s);
+    run(prof, s, name, 2.0 * P * cv.Cout * cv.Cin * cv.K, 4.0 * P * (cv.Cin + cv.Cout),
+        [&] { launch_conv(cfg_.math_mode, a, B, cv.K, cv.tile, s); });
   };
 
   // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1
   for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
     const Flow& F = flows_[f];
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
-    conv(F.start, xs, (int64_t)C2 * Th, hb, msq);
+    conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq);
     for (int l = 0; l < L; ++l) {
-      conv(F.in_layers[l], hb, 0, xin, nullptr);                 // wavenet.py:101
-      launch_glow_gate(xin, acts, B, H, Th, s);                  // :108
-      conv(F.res_skip[l], acts, 0, rs, nullptr);                 // :109
-      launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s);  // :110-115
+      conv("glow_wn_in", F.in_layers[l], hb, 0, xin, nullptr);                   // wavenet.py:101
+      run(prof, s, "glow_gate", 0.0, 12.0 * P * H, [&] { launch_glow_gate(xin, acts, B, H, Th, s); });  // :108
+      conv("glow_wn_res_skip", F.res_skip[l], acts, 0, rs, nullptr);             // :109
+      run(prof, s, "glow_wn_update", 0.0, 24.0 * P * H,
+          [&] { launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s); });  // :110-115
     }
-    conv(F.end, skip, 0, out, nullptr);                          // glow.py:214
+    conv("glow_end", F.end, skip, 0, out, nullptr);                             // glow.py:214
     GlowTailArgs ta{};
     ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
     ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
-    launch_glow_tail(ta, B, s);
+    run(prof, s, "glow_tail", 0.0, 16.0 * P * C2, [&] { launch_glow_tail(ta, B, s); });
   }
   if (nsq > 1) {
-    launch_glow_unsqueeze(xs, msq, y, B, C, Th, nsq, s);
+    run(prof, s, "glow_unsqueeze", 0.0, 8.0 * P * C2 + 4.0 * P,
+        [&] { launch_glow_unsqueeze(xs, msq, y, B, C, Th, nsq, s); });
   } else {
     TTS_HIP_CHECK(hipMemcpyAsync(y, xs, plane * C2 * sizeof(float), hipMemcpyDeviceToDevice, s));
   }

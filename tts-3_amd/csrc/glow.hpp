@@ -40,7 +40,9 @@ class GlowDecoder {
   ~GlowDecoder();
   GlowDecoder(const GlowDecoder&) = delete;
   GlowDecoder& operator=(const GlowDecoder&) = delete;
-  void reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s);
+  void reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s,
+               Profiler* prof = nullptr);
+  int device() const { return device_; }
 
  private:
   struct Conv {

@@ -120,6 +120,11 @@ SIGNATURES = {
     "tts_glow_decoder_forward": (
         c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]
     ),
+    "tts_glow_decoder_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
     "tts_op_conv1d": (
         c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     ),

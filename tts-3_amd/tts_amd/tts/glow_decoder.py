@@ -254,6 +254,24 @@ class Decoder(nn.Module):
             N.call("tts_glow_decoder_forward", h, N.ptr(x), N.ptr(m), B, C, T, 1, N.ptr(y), N.stream_ptr(dev))
         return y, None
 
+    def profile(self, x: torch.Tensor, x_mask: torch.Tensor):
+        """One reverse pass with a hipEvent pair around every launch: (y, [{name, flops, bytes, ms}])."""
+        h = self._native_handle()
+        dev = self._device()
+        x = x.to(device=dev, dtype=torch.float32).contiguous()
+        B, C, T = x.shape
+        m = x_mask.to(device=dev, dtype=torch.float32).reshape(B, T).contiguous()
+        Tq = (T // self.num_squeeze) * self.num_squeeze if self.num_squeeze > 1 else T
+        y = torch.empty(B, C, Tq, device=dev)
+        cap = 2048
+        recs = (N.TtsLaunchRecord * cap)()
+        n = ctypes.c_int(0)
+        N.call("tts_glow_decoder_forward_profiled", h, N.ptr(x), N.ptr(m), B, C, T, 1, N.ptr(y), N.stream_ptr(dev),
+               recs, cap, ctypes.byref(n))
+        rows = [{"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
+                for i in range(min(n.value, cap))]
+        return y, rows
+
     def store_inverse(self):  # decoder.py:139-141
         for f in self.flows:
             f.store_inverse()
