@@ -5,6 +5,30 @@
 
 namespace tts {
 
+// ---- raw buffer access (CDNA buffer resource descriptors) -------------------------------
+// A 128-bit descriptor in SGPRs + a 32-bit per-lane byte offset + a wave-uniform soffset: no
+// 64-bit address arithmetic per access, and the hardware range check returns 0 for loads /
+// drops stores whose offset is >= num_records.  OOB_OFF marks a lane's access invalid (callers
+// keep voffset + soffset < 2^32, i.e. every addressed plane < 2 GiB; checked on the host).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned OOB_OFF = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ void bstore(rsrc_t r, float v, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, 0);
+}
+// leaky_relu for 0 < slope <= 1 (slope 1 = identity): max(x, slope*x), 2 VALU
+__device__ __forceinline__ float lrelu2(float x, float slope) { return fmaxf(x, x * slope); }
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 // LDS float offset of channel quad q (0/1) of input row r in group g.  The quad index is
 // XOR-swizzled with bit 3 of the row: every ds_read_b128 lane group (16 lanes, rows
 // r0 + {0-3,12-15,20-27} or {4-11,16-19,28-31}) then hits 16 distinct 16-byte bank slots
@@ -31,58 +55,53 @@ __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x
   const int Cout = a.Cout;
   const int Tout = a.Tout;
   const int zmode = a.zmode;
-  const float* __restrict__ bias = a.bias;
-  const float* cvec = a.cvec;
-  const float* mask = a.mask;
-  const float* res = a.res;
-  const float* zin = (zmode >= 2) ? a.z : nullptr;
-  float* out = (zmode == 0) ? a.y : a.z;
-
-  // per-batch bases (wave-uniform) + 32-bit in-item offsets: one VGPR per gathered address
+  const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;  // bytes of one batch item
   const size_t item = (size_t)b * Cout * Tout;
-  const float* rb = res ? res + item : nullptr;
-  const float* zb = zin ? zin + item : nullptr;
-  float* ob = out + item;
-  const float* cb = cvec ? cvec + (size_t)b * Cout : nullptr;
-  const float* mb = mask ? mask + (size_t)b * Tout : nullptr;
-  // per 32x32 block: gather every value this thread reads, then compute and store
-  // (TM*TN memory round trips per thread)
+  const bool has_res = a.res != nullptr;
+  const bool has_z = zmode >= 2;
+  const rsrc_t rres = make_rsrc(has_res ? a.res + item : a.bias, has_res ? plane : 0u);
+  const rsrc_t rz = make_rsrc(a.z + (a.z ? item : 0), a.z ? plane : 0u);
+  const rsrc_t rout = make_rsrc((zmode == 0 ? a.y : a.z) + item, plane);
+  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * Cout : a.bias, a.cvec ? (unsigned)Cout * 4u : 0u);
+  const rsrc_t rmask = make_rsrc(a.mask ? a.mask + (size_t)b * Tout : a.bias, a.mask ? (unsigned)Tout * 4u : 0u);
+  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
+  const float oslope = a.out_slope;
+  const unsigned rowb = (unsigned)Tout * 4u;
+  // per 32x32 block: gather every value this thread reads, then compute and store.  Every
+  // range-checked offset is in the per-lane voffset (lane row cobase + m*32 + 4*half, column t;
+  // register r adds row (r&3) + 8*(r>>2)).
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
     float bv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const int cc = co < Cout ? co : 0;
-      float v = bias[cc];
-      if (cb) v += cb[cc];
-      bv[r] = v;
+      bv[r] = bload(rbias, (unsigned)co * 4u, 0u) + (a.cvec ? bload(rcv, (unsigned)co * 4u, 0u) : 0.f);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
       const int t = tbase + n * 32 + l32;
-      const float mv = mb ? mb[t < Tout ? t : 0] : 1.f;
+      const int row0 = cobase + m * 32 + 4 * half;
+      // rows >= Cout land past the plane through the row term; columns >= Tout are marked OOB
+      const unsigned voff = (t < Tout) ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+      const float mv = a.mask ? bload(rmask, (t < Tout ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
+      unsigned vo[16];
       float rv[16], zv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        const bool ok = co < Cout && t < Tout;
-        const int off = ok ? co * Tout + t : 0;
-        rv[r] = rb ? rb[off] : 0.f;
-        zv[r] = zb ? zb[off] : 0.f;
+        vo[r] = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
+        rv[r] = has_res ? bload(rres, vo[r], 0u) : 0.f;
+        zv[r] = has_z ? bload(rz, vo[r], 0u) : 0.f;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (co < Cout && t < Tout) {
-          float v = acc[m][n][r] + bv[r];
-          if (mb) v *= mv;
-          v = lrelu(v, a.out_slope);
-          if (rb) v += rv[r];
-          if (zmode == 2) v = zv[r] + v;
-          else if (zmode == 3) v = (zv[r] + v) / a.zdiv;
-          ob[co * Tout + t] = v;
-        }
+        float v = acc[m][n][r] + bv[r];
+        if (a.mask) v *= mv;
+        v = lrelu2(v, oslope);
+        if (has_res) v += rv[r];
+        if (zmode == 2) v = zv[r] + v;
+        else if (zmode == 3) v = (zv[r] + v) / a.zdiv;
+        bstore(rout, v, vo[r], 0u);
       }
     }
   }

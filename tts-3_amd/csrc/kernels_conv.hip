@@ -71,12 +71,15 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
   const int Cin = a.Cin;
   const int nc = a.n_chunks;
 
-  const float* __restrict__ xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  // x of batch item b; one buffer descriptor per chunk (scalar ops), every range-checked
+  // offset in the per-lane voffset: zero rows and channels >= Cin read 0 through the hardware
+  // range check instead of per-element selects
+  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  const unsigned chb = (unsigned)Tin * 4u;  // bytes per channel row
 
-  // ---- staging units (chunk invariant): unit u -> group g, row r, channel quad q
-  int uoff[C::UPT];   // element offset of channel (8g+4q) at the clamped source time
-  int uch[C::UPT];    // channel index 8g+4q within the chunk, or huge when the row is invalid
-  int ulds[C::UPT];   // LDS float offset of the row's quad
+  // staging units (chunk invariant): unit u -> channel quad q, row r, group g
+  unsigned uvoff[C::UPT];  // byte offset of channel (8g+4q) at the clamped source time, or OOB
+  int ulds[C::UPT];        // LDS offset of the row's quad
 #pragma unroll
   for (int i = 0; i < C::UPT; ++i) {
     const int u = tid + i * 256;
@@ -88,27 +91,18 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
     const bool ok = (g < G) && ts >= 0 && ts < Tout;
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
-    uoff[i] = (8 * g + 4 * q) * Tin + src;
-    uch[i] = ok ? 8 * g + 4 * q : 0x40000000;
+    uvoff[i] = ok ? (unsigned)(8 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
     ulds[i] = (g < G) ? xlds_off(g, r, q, C::XROWS) : -1;
   }
 
   f32x4 xreg[C::UPT];
   auto load_x = [&](int c) {
     const int c0 = c * C::CK;
-    const float* xc = xb + (size_t)c0 * Tin;
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
 #pragma unroll
     for (int i = 0; i < C::UPT; ++i) {
-      float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ch = uch[i] + j;                       // channel within chunk
-        const bool ok = (c0 + ch) < Cin;
-        const int off = ok ? uoff[i] + j * Tin : 0;      // always in bounds
-        const float x = xc[off];
-        v[j] = ok ? x : 0.f;
-      }
-      xreg[i] = f32x4{v[0], v[1], v[2], v[3]};
+      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
     }
   };
   auto store_x = [&](int buf) {
@@ -118,20 +112,24 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
     for (int i = 0; i < C::UPT; ++i) {
       if (ulds[i] >= 0) {
         f32x4 v = xreg[i];
-        v[0] = lrelu(v[0], slope); v[1] = lrelu(v[1], slope);
-        v[2] = lrelu(v[2], slope); v[3] = lrelu(v[3], slope);
+        v[0] = lrelu2(v[0], slope); v[1] = lrelu2(v[1], slope);
+        v[2] = lrelu2(v[2], slope); v[3] = lrelu2(v[3], slope);
         *reinterpret_cast<f32x4*>(xl + ulds[i]) = v;
       }
     }
   };
 
   // ---- A fragment streams: one per m-block of this wave, step index = c8 * K + k
-  const f32x4* ap[TM];
+  // (descriptor per m-block from wave-uniform values; step offsets go in the scalar soffset,
+  // the stream is padded so no range check is needed)
+  rsrc_t ra[TM];
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
-    const int mb = mt * (BM / 32) + wm * TM + m;
-    ap[m] = reinterpret_cast<const f32x4*>(a.w) + ((size_t)mb * nc * G * K) * 64 + lane;
+    const int mb = mt * (BM / 32) + wmu * TM + m;
+    ra[m] = make_rsrc(a.w + ((size_t)mb * nc * G * K) * 256, 0xFFFFFFFFu);
   }
+  const unsigned avoff = (unsigned)lane * 16u;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -146,7 +144,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
 #pragma unroll
   for (int p = 0; p < PD; ++p)
 #pragma unroll
-    for (int m = 0; m < TM; ++m) ar[p][m] = ap[m][(size_t)p * 64];
+    for (int m = 0; m < TM; ++m) ar[p][m] = bload4(ra[m], avoff, (unsigned)p * 1024u);
 
   // B read of (group g, tap k) for this lane's TN columns; quad = lane half
   auto read_b = [&](const float* xl, int g, int k, f32x4* dst) {
@@ -174,7 +172,7 @@ __global__ __launch_bounds__(256) void conv1d_mfma_kernel(Conv1dArgs a) {
         const int s = (c * G + g) * K + k;  // global step of this (group, tap)
         // prefetch: A for step s+PD from L2 (the stream is padded), B for step s+1 from LDS
 #pragma unroll
-        for (int m = 0; m < TM; ++m) ar[PD][m] = ap[m][(size_t)(s + PD) * 64];
+        for (int m = 0; m < TM; ++m) ar[PD][m] = bload4(ra[m], avoff, (unsigned)(s + PD) * 1024u);
         const bool bnext_here = (k + 1 < K) || (g + 1 < G);
         if (bnext_here) read_b(xl, (k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
         // keep the prefetches ahead of this step's MFMAs (the scheduler otherwise sinks them

@@ -75,12 +75,15 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
   const int Cin = a.Cin;
   const int nc = a.n_chunks;
 
-  const float* __restrict__ xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  // x of batch item b; one buffer descriptor per chunk (scalar ops), every range-checked
+  // offset in the per-lane voffset: zero rows and channels >= Cin read 0 through the hardware
+  // range check instead of per-element selects
+  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  const unsigned chb = (unsigned)Tin * 4u;  // bytes per channel row
 
-  // staging units: u -> channel quad q (4 channels), row r, group g
-  int uoff[C::UPT];
-  int uch[C::UPT];
-  int ulds[C::UPT];
+  // staging units (chunk invariant): unit u -> channel quad q, row r, group g
+  unsigned uvoff[C::UPT];  // byte offset of channel (16g+4q) at the clamped source time, or OOB
+  int ulds[C::UPT];        // LDS offset of the row's quad
 #pragma unroll
   for (int i = 0; i < C::UPT; ++i) {
     const int u = tid + i * 256;
@@ -92,26 +95,18 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
     const bool ok = (g < G) && ts >= 0 && ts < Tout;
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
-    uoff[i] = (16 * g + 4 * q) * Tin + src;
-    uch[i] = ok ? 16 * g + 4 * q : 0x40000000;
+    uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
     ulds[i] = (g < G) ? (g * C::XROWS + r) * X6_ROWB + 8 * q : -1;
   }
 
   f32x4 xreg[C::UPT];
   auto load_x = [&](int c) {
     const int c0 = c * C::CK;
-    const float* xc = xb + (size_t)c0 * Tin;
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
 #pragma unroll
     for (int i = 0; i < C::UPT; ++i) {
-      float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ch = uch[i] + j;
-        const bool ok = (c0 + ch) < Cin;
-        const float x = xc[ok ? uoff[i] + j * Tin : 0];
-        v[j] = ok ? x : 0.f;
-      }
-      xreg[i] = f32x4{v[0], v[1], v[2], v[3]};
+      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
     }
   };
   auto store_x = [&](int buf) {
@@ -124,7 +119,7 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           unsigned short h0, h1, h2;
-          split3(lrelu(xreg[i][j], slope), h0, h1, h2);
+          split3(lrelu2(xreg[i][j], slope), h0, h1, h2);
           p0[j] = h0;
           p1[j] = h1;
           p2[j] = h2;
@@ -137,12 +132,15 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
   };
 
   // A streams: f32x4 units, fragment (mb, step s, piece p) at ((mb*S + s)*3 + p)*64 + lane
-  const f32x4* ap[TM];
+  // (descriptor per m-block from wave-uniform values, step/piece offsets in the scalar soffset)
+  rsrc_t ra[TM];
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
-    const int mb = mt * (BM / 32) + wm * TM + m;
-    ap[m] = reinterpret_cast<const f32x4*>(a.w) + ((size_t)mb * nc * G * K) * 192 + lane;
+    const int mb = mt * (BM / 32) + wmu * TM + m;
+    ra[m] = make_rsrc(a.w + ((size_t)mb * nc * G * K) * 768, 0xFFFFFFFFu);
   }
+  const unsigned avoff = (unsigned)lane * 16u;
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -158,7 +156,7 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) ar[p][m][q] = ap[m][((size_t)p * 3 + q) * 64];
+      for (int q = 0; q < 3; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * 3 + q) * 1024u);
 
   auto read_b = [&](const unsigned char* xl, int g, int k, f32x4 (*dst)[3]) {
 #pragma unroll
@@ -188,7 +186,7 @@ __global__ __launch_bounds__(256) void conv1d_x6_kernel(Conv1dArgs a) {
 #pragma unroll
         for (int m = 0; m < TM; ++m)
 #pragma unroll
-          for (int q = 0; q < 3; ++q) ar[PD][m][q] = ap[m][((size_t)(s + PD) * 3 + q) * 64];
+          for (int q = 0; q < 3; ++q) ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((s + PD) * 3 + q) * 1024u);
         const bool bnext_here = (k + 1 < K) || (g + 1 < G);
         if (bnext_here) read_b(xl, (k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
         __builtin_amdgcn_sched_barrier(0);
