@@ -1,12 +1,8 @@
+# Tile sweep (both math modes) on the benchmark's conv shapes; logs under gpurun_out/.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-tail -3 gpurun_out/pytest_gpu.log
-if [ $rc -le 1 ]; then
-  timeout -k 10 900 python scripts/tune_conv.py > gpurun_out/tune.log 2>&1
-  echo "tune rc=$?"
-  cat gpurun_out/tune.log
-fi
+for m in ${TUNE_MODES:-fp32x6 fp32}; do
+  timeout -k 10 400 python scripts/tune_conv.py $m $TUNE_ONLY > gpurun_out/tune_$m.log 2>&1 || exit 1
+  grep -v amdgpu.ids gpurun_out/tune_$m.log
+done

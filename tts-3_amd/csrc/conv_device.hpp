@@ -45,38 +45,35 @@ __device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
 // so every value this thread reads is loaded BEFORE its first store: otherwise the compiler
 // cannot hoist a load above the previous element's store and each element pays a full memory
 // round trip (measured: residual convs 2x slower).
-template <int TM, int TN>
-__device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
-                                              int tbase, int cobase, int lane) {
-  // copy the argument block: a store through `out` could alias it in the compiler's view
-  const Conv1dArgs a = args;
+template <int TM, int TN, bool RES, int ZM>
+__device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
+                                                   int tbase, int cobase, int lane) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int Cout = a.Cout;
   const int Tout = a.Tout;
-  const int zmode = a.zmode;
   const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;  // bytes of one batch item
   const size_t item = (size_t)b * Cout * Tout;
-  const bool has_res = a.res != nullptr;
-  const bool has_z = zmode >= 2;
-  const rsrc_t rres = make_rsrc(has_res ? a.res + item : a.bias, has_res ? plane : 0u);
-  const rsrc_t rz = make_rsrc(a.z + (a.z ? item : 0), a.z ? plane : 0u);
-  const rsrc_t rout = make_rsrc((zmode == 0 ? a.y : a.z) + item, plane);
+  const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
+  const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
+  const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
   const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * Cout : a.bias, a.cvec ? (unsigned)Cout * 4u : 0u);
   const rsrc_t rmask = make_rsrc(a.mask ? a.mask + (size_t)b * Tout : a.bias, a.mask ? (unsigned)Tout * 4u : 0u);
   const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
+  const bool has_mask = a.mask != nullptr;
   const float oslope = a.out_slope;
+  const float zdiv = a.zdiv;
   const unsigned rowb = (unsigned)Tout * 4u;
   // per 32x32 block: gather every value this thread reads, then compute and store.  Every
   // range-checked offset is in the per-lane voffset (lane row cobase + m*32 + 4*half, column t;
-  // register r adds row (r&3) + 8*(r>>2)).
+  // register r adds row (r&3) + 8*(r>>2)); an absent cvec reads 0 through a 0-byte descriptor.
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
     float bv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int co = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      bv[r] = bload(rbias, (unsigned)co * 4u, 0u) + (a.cvec ? bload(rcv, (unsigned)co * 4u, 0u) : 0.f);
+      const unsigned co = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
+      bv[r] = bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
@@ -84,26 +81,44 @@ __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x
       const int row0 = cobase + m * 32 + 4 * half;
       // rows >= Cout land past the plane through the row term; columns >= Tout are marked OOB
       const unsigned voff = (t < Tout) ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-      const float mv = a.mask ? bload(rmask, (t < Tout ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
+      const float mv = has_mask ? bload(rmask, (t < Tout ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
       unsigned vo[16];
       float rv[16], zv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         vo[r] = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-        rv[r] = has_res ? bload(rres, vo[r], 0u) : 0.f;
-        zv[r] = has_z ? bload(rz, vo[r], 0u) : 0.f;
+        if (RES) rv[r] = bload(rres, vo[r], 0u);
+        if (ZM >= 2) zv[r] = bload(rz, vo[r], 0u);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float v = acc[m][n][r] + bv[r];
-        if (a.mask) v *= mv;
+        float v = (acc[m][n][r] + bv[r]) * mv;  // mv = 1 without a mask (exact)
         v = lrelu2(v, oslope);
-        if (has_res) v += rv[r];
-        if (zmode == 2) v = zv[r] + v;
-        else if (zmode == 3) v = (zv[r] + v) / a.zdiv;
+        if (RES) v += rv[r];
+        if (ZM == 2) v = zv[r] + v;
+        if (ZM == 3) v = (zv[r] + v) / zdiv;
         bstore(rout, v, vo[r], 0u);
       }
     }
+  }
+}
+
+// The per-element options are template parameters (one uniform dispatch per tile), so the
+// unrolled epilogue carries no per-element branches.
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
+                                              int tbase, int cobase, int lane) {
+  // copy the argument block: a store through `out` could alias it in the compiler's view
+  const Conv1dArgs a = args;
+  const int zm = a.zmode <= 1 ? 0 : a.zmode;
+  if (a.res) {
+    if (zm == 0) conv_epilogue_impl<TM, TN, true, 0>(a, acc, b, tbase, cobase, lane);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, true, 2>(a, acc, b, tbase, cobase, lane);
+    else conv_epilogue_impl<TM, TN, true, 3>(a, acc, b, tbase, cobase, lane);
+  } else {
+    if (zm == 0) conv_epilogue_impl<TM, TN, false, 0>(a, acc, b, tbase, cobase, lane);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, false, 2>(a, acc, b, tbase, cobase, lane);
+    else conv_epilogue_impl<TM, TN, false, 3>(a, acc, b, tbase, cobase, lane);
   }
 }
 

@@ -513,13 +513,13 @@ void launch_convT_t(const ConvTArgs& a, int B, hipStream_t s) {
 // Tile choice per conv shape, from the round-1 sweep on MI355X (profiles/r01_tune_conv.log,
 // HiFiGAN-v1 shapes at B=32 x 1034 frames).  `res`: the epilogue adds a residual.
 int conv1d_tile_for(int Cout, int K, int Cin, int dil, bool res) {
+  (void)res;
   if ((K - 1) * dil > (K - 1) * DMAX) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
   if (Cout > 64) {
-    if (Cin % 32 != 0) return K <= 3 ? 4 : 0;      // conv_pre (Cin 80), Glow start
-    if (K <= 3) return (res && Cout <= 128) ? 10 : 4;
-    return res ? 3 : 11;
+    if (Cin % 32 != 0) return K <= 3 ? 4 : 0;  // conv_pre (Cin 80), Glow start
+    return (K >= 11 && Cout <= 128) ? 3 : 11;
   }
-  if (Cout > 32) return (K <= 3 || res) ? 10 : 1;
+  if (Cout > 32) return 10;
   return K >= 11 ? 2 : 8;
 }
 

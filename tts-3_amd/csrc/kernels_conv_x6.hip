@@ -237,6 +237,11 @@ constexpr ConvTile kX6Tiles[] = {
     {32, 256, 1, 2, 32, 1},   // 5
     {64, 256, 2, 2, 32, 1},   // 6
     {128, 128, 2, 2, 16, 2},  // 7
+    {64, 128, 2, 1, 32, 2},   // 8  tile 4, A prefetched 2 steps ahead
+    {64, 256, 2, 2, 32, 2},   // 9  4 waves along t, 2 column blocks each
+    {64, 256, 2, 2, 16, 2},   // 10
+    {32, 256, 1, 2, 32, 2},   // 11 tile 5, prefetch 2
+    {64, 128, 2, 1, 32, 3},   // 12 prefetch 3
 };
 constexpr int kNumX6Tiles = sizeof(kX6Tiles) / sizeof(kX6Tiles[0]);
 
@@ -264,6 +269,11 @@ void launch_x6_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
     case 5: launch_x6_t<K, 32, 256, 1, 2, 2, 1, false>(a, B, s); break;
     case 6: launch_x6_t<K, 64, 256, 2, 2, 2, 1, false>(a, B, s); break;
     case 7: launch_x6_t<K, 128, 128, 2, 2, 1, 2, false>(a, B, s); break;
+    case 8: launch_x6_t<K, 64, 128, 2, 1, 2, 2, false>(a, B, s); break;
+    case 9: launch_x6_t<K, 64, 256, 2, 2, 2, 2, false>(a, B, s); break;
+    case 10: launch_x6_t<K, 64, 256, 2, 2, 1, 2, false>(a, B, s); break;
+    case 11: launch_x6_t<K, 32, 256, 1, 2, 2, 2, false>(a, B, s); break;
+    case 12: launch_x6_t<K, 64, 128, 2, 1, 2, 3, false>(a, B, s); break;
     default: throw Error(3, "conv1d(x6): bad tile index " + std::to_string(tile));
   }
 }
@@ -276,14 +286,14 @@ ConvTile conv1d_x6_tile(int idx) {
 
 int conv1d_x6_num_tiles() { return kNumX6Tiles; }
 
-// Tile choice per conv shape from the round-1 MI355X sweep (profiles/r01_tune_conv_fp32x6.log).
+// Tile choice per conv shape from the round-1 MI355X sweep (profiles/r01_tune_conv_fp32x6.log,
+// buffer-addressed kernels).  Any tile is correct for any Cin: channels past Cin read 0.
 int conv1d_x6_tile_for(int Cout, int K, int Cin, int dil, bool res) {
   (void)res;
   if ((K - 1) * dil > (K - 1) * 5) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
-  if (Cin % 32 != 0) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);                // conv_pre (80 ch)
-  if (Cout > 128 && K >= 7) return 3;
-  if (Cout > 32) return 4;
-  return K <= 3 ? 4 : 5;
+  if (Cout > 64) return (K >= 11 || Cin % 32 != 0) ? 7 : 3;
+  if (Cout > 32) return K <= 3 ? 10 : 1;
+  return 2;
 }
 
 void launch_conv1d_x6(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
