@@ -30,8 +30,19 @@ import torch.distributed as dist  # noqa: E402
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
 # ceiling of each math mode in algorithmic fp32 FLOP/s: fp32x6 issues 6 bf16 MFMA products
-# per fp32 multiply-accumulate (include/tts_mi355x.h TTS_MATH_FP32_X6)
-MODE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS / 6.0}
+# per fp32 multiply-accumulate, f16x3 3 fp16 products (same MFMA rate as bf16); see
+# include/tts_mi355x.h TTS_MATH_*
+MODE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS / 6.0, "f16x3": BF16_PEAK_TFLOPS / 3.0}
+PEAK_BASIS = {
+    "fp32": "fp32 MFMA 157.3 TF",
+    "fp32x6": "bf16 dense MFMA 2.5 PF / 6 products per fp32 MAC",
+    "f16x3": "fp16 dense MFMA 2.5 PF / 3 products per fp32 MAC",
+}
+DTYPE = {
+    "fp32": "fp32",
+    "fp32x6": "fp32 (bf16x6 split on bf16 MFMA, fp32 accumulate)",
+    "f16x3": "fp32 (power-of-2 scaled fp16 hi/lo split on fp16 MFMA, fp32 accumulate)",
+}
 HBM_PEAK_GBS = 8000.0
 SAMPLE_RATE = 22050
 METRIC = "audio samples/sec + RTF, HiFiGAN-v1 22.05kHz 80-mel, batch 32 @ 1/2/4/8 GPU"
@@ -48,7 +59,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     p.add_argument("--comm", action="store_true",
                    help="also time an RCCL scatter of mels / gather of wavs from rank 0 (reported separately)")
-    p.add_argument("--math-mode", default="fp32x6", choices=["fp32", "fp32x6"],
+    p.add_argument("--math-mode", default="f16x3", choices=sorted(MODE_PEAK),
                    help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
     p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
     p.add_argument("--no-glow", action="store_true", help="skip the Glow-TTS decoder measurement")
@@ -273,7 +284,7 @@ def main():
     alt = None
     gens = {a.math_mode: g}
     if not a.no_alt:
-        other = "fp32" if a.math_mode == "fp32x6" else "fp32x6"
+        other = "fp32" if a.math_mode != "fp32" else "fp32x6"
         g2 = build_generator(other, dev)
         g2.reserve(B, T)
         ms2 = time_steps(g2, mel, max(3, a.steps // 2), 1, dev, world)
@@ -288,7 +299,9 @@ def main():
 
     glow = None
     if rank == 0 and not a.no_glow:
-        glow = glow_bench(dev, a.math_mode, cpu=(world == 1 and not a.no_cpu_baseline))
+        # the Glow decoder implements fp32 and fp32x6 (TTS_MATH_FP32_F16X3 is HiFiGAN-only)
+        glow_mode = "fp32x6" if a.math_mode == "f16x3" else a.math_mode
+        glow = glow_bench(dev, glow_mode, cpu=(world == 1 and not a.no_cpu_baseline))
 
     if rank == 0:
         rec = {
@@ -302,7 +315,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if a.math_mode == "fp32" else "fp32 (bf16x6 split on bf16 MFMA, fp32 accumulate)",
+            "dtype": DTYPE[a.math_mode],
             "math_mode": a.math_mode,
             "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
             "config": {
@@ -321,7 +334,7 @@ def main():
                 "launches_per_step": fam["n"],
                 "achieved": achieved,
                 "peak": MODE_PEAK[a.math_mode],
-                "peak_basis": "fp32 MFMA 157.3 TF" if a.math_mode == "fp32" else "bf16 dense MFMA 2.5 PF / 6 products per fp32 MAC",
+                "peak_basis": PEAK_BASIS[a.math_mode],
                 "unit": "TFLOP/s",
                 "frac": achieved / MODE_PEAK[a.math_mode],
                 "traffic": traffic,

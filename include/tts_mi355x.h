@@ -48,9 +48,18 @@ extern "C" {
  *   TTS_MATH_FP32     v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulation
  *   TTS_MATH_FP32_X6  each fp32 operand split exactly into 3 bf16 pieces, the 6 significant
  *                     cross products accumulated in fp32 on v_mfma_f32_32x32x16_bf16
- *                     (dropped terms < 2^-26 relative; 2.67x the fp32-MFMA ceiling) */
+ *                     (dropped terms < 2^-26 relative; 2.67x the fp32-MFMA ceiling)
+ *   TTS_MATH_FP32_F16X3  each operand, scaled by an exact power of two so its max-abs lies in
+ *                     [2^13, 2^14), split into hi = fp16(x) and lo = fp16(x - hi); hi*hi, hi*lo
+ *                     and lo*hi accumulated in fp32 on v_mfma_f32_32x32x16_f16 (22 significant
+ *                     bits per operand, dropped term ~2^-22 relative; 5.3x the fp32-MFMA
+ *                     ceiling).  The
+ *                     scales come from max-abs statistics each producing kernel records; the
+ *                     HiFiGAN executor runs conv_pre (user input, no statistics) in FP32_X6.
+ *                     HiFiGAN only: the Glow decoder rejects it (TTS_ERR_UNSUPPORTED). */
 #define TTS_MATH_FP32 0
 #define TTS_MATH_FP32_X6 1
+#define TTS_MATH_FP32_F16X3 2
 
 #define TTS_MAX_UPSAMPLES 8
 #define TTS_MAX_KERNELS 4
@@ -87,7 +96,7 @@ typedef struct TtsHifiganCfg {
   int inference_padding;                /* default 5 (:173) */
   int cond_channels;                    /* 0 = no cond_layer (:227-228) */
   int conv_post_bias;                   /* default 1 (:177) */
-  int math_mode;                        /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
+  int math_mode;                        /* TTS_MATH_FP32 (default), _X6 or _F16X3 */
 } TtsHifiganCfg;
 
 /* Number of host weight tensors create() expects, and the element count of tensor idx.
@@ -189,7 +198,7 @@ typedef struct TtsConv1dDesc {
   float in_slope, out_slope;
   int zmode;
   float zdiv;
-  int math_mode; /* TTS_MATH_FP32 / TTS_MATH_FP32_X6 */
+  int math_mode; /* TTS_MATH_FP32 / TTS_MATH_FP32_X6 / TTS_MATH_FP32_F16X3 */
 } TtsConv1dDesc;
 int tts_op_conv1d(const TtsConv1dDesc* d, const float* d_x, const float* h_w, const float* h_b,
                   const float* d_res, float* d_y, float* d_z, void* hip_stream);

@@ -44,7 +44,8 @@ def main():
         d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, 0, 0.1, 1.0 if use_res else 0.1, 0, 1.0, N.MATH_MODES[mode])
         ref = None
         rows = []
-        for tile in range(ntiles):
+        tiles = [int(t) for t in os.environ["TUNE_TILES"].split(",")] if os.environ.get("TUNE_TILES") else range(ntiles)
+        for tile in tiles:
             y = torch.empty(B, Cout, T, device=dev)
             ms = ctypes.c_float(0)
             st = N.lib().tts_op_conv1d_bench(ctypes.byref(d), N.ptr(x), N.ptr(w), N.ptr(bias), N.ptr(res), N.ptr(y),

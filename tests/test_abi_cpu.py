@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 101
+    assert N.lib().tts_abi_version() == 102
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -163,6 +163,19 @@ def test_glow_config_validation():
     assert b"num_splits" in N.lib().tts_last_error()
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, N.MATH_MODES["f16x3"])
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    assert b"F16X3" in N.lib().tts_last_error()
+
+
+def test_math_modes_and_tile_tables():
+    lib = N.lib()
+    assert N.MATH_MODES == {"fp32": 0, "fp32x6": 1, "f16x3": 2}
+    for m in N.MATH_MODES.values():
+        assert lib.tts_op_conv1d_num_tiles(m) >= 3
+    assert lib.tts_op_conv1d_num_tiles(7) == -N.TTS_ERR_INVALID
+    g = HifiganGenerator(**V1, math_mode="f16x3")
+    assert g._cfg.math_mode == 2
 
 
 def test_null_arguments_return_invalid():

@@ -32,6 +32,8 @@ def _rng(seed):
 
 
 # ----------------------------------------------------------------------------- conv1d
+MODES = ["fp32", "fp32x6", "f16x3"]  # TTS_MATH_* (f16x3: HiFiGAN executor and the conv op only)
+
 CONV_CASES = [
     # B, Cin, Cout, T, K, dil, rep, in_slope, out_slope, res, zmode
     (2, 80, 512, 37, 7, 1, 5, 1.0, 1.0, False, 0),     # conv_pre with replicate padding
@@ -50,7 +52,7 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("case", CONV_CASES, ids=[f"c{i}" for i in range(len(CONV_CASES))])
 def test_op_conv1d(cuda_device, case, mode):
     B, Cin, Cout, T, K, dil, rep, s_in, s_out, use_res, zmode = case
@@ -137,7 +139,7 @@ def build(cfg, seed, device, math_mode="fp32"):
     return g.to(device)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name,meta,arr", HIFI, ids=[h[0] for h in HIFI])
 def test_generator_vs_reference_goldens(cuda_device, name, meta, arr, mode):
     cfg = meta["config"]
@@ -203,7 +205,7 @@ def test_profiled_forward_records(cuda_device):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+@pytest.mark.parametrize("mode", MODES)
 def test_benchmark_size_properties(cuda_device, mode):
     """Config 2 of BASELINE.json: B=32 x 1024 frames, HiFiGAN-v1, fp32."""
     sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
@@ -225,15 +227,17 @@ def test_benchmark_size_properties(cuda_device, mode):
     assert_close_fp32(out[17:18].cpu(), ref, "B=32 item 17 vs fp64 oracle")
 
 
-def test_x6_accuracy_not_worse_than_fp32(cuda_device):
-    """The bf16x6 split is fp32-faithful: its error vs the fp64 reference matches exact-fp32 MFMA."""
+def test_split_modes_accuracy_not_worse_than_fp32(cuda_device):
+    """The bf16x6 and scaled fp16 hi/lo splits are fp32-faithful: their error vs the fp64
+    reference matches exact-fp32 MFMA (and the reference's own fp32 CPU forward)."""
     name, meta, arr = [h for h in HIFI if h[0] == "hifigan_v1_b2_t32"][0]
     errs = {}
-    for mode in ("fp32", "fp32x6"):
+    for mode in MODES:
         g = build(meta["config"], meta["seed"], cuda_device, mode)
         out = g.inference(torch.from_numpy(arr["mel"]).to(cuda_device)).cpu().numpy()
         errs[mode] = (max_abs(out, arr["out_ref_fp64"]), rel_rms(out, arr["out_ref_fp64"]))
     ref32 = (max_abs(arr["out_ref_fp32"], arr["out_ref_fp64"]), rel_rms(arr["out_ref_fp32"], arr["out_ref_fp64"]))
     print("max|d|, rel-RMS vs fp64:", errs, "reference fp32 CPU:", ref32)
-    assert errs["fp32x6"][1] <= 2.0 * max(errs["fp32"][1], ref32[1])
-    assert errs["fp32x6"][0] <= 2.0 * max(errs["fp32"][0], ref32[0])
+    for mode in ("fp32x6", "f16x3"):
+        assert errs[mode][1] <= 2.0 * max(errs["fp32"][1], ref32[1]), mode
+        assert errs[mode][0] <= 2.0 * max(errs["fp32"][0], ref32[0]), mode

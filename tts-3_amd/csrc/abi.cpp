@@ -55,7 +55,7 @@ struct TmpDev {
   explicit TmpDev(const float* host, size_t n) {
     if (n == 0) return;
     if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) throw tts::Error(4, "hipMalloc failed");
-    TTS_HIP_CHECK(hipMemcpy(p, host, n * sizeof(float), hipMemcpyHostToDevice));
+    if (host) TTS_HIP_CHECK(hipMemcpy(p, host, n * sizeof(float), hipMemcpyHostToDevice));
   }
   ~TmpDev() {
     if (p) (void)hipFree(p);
@@ -66,7 +66,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 101; }
+int tts_abi_version(void) { return 102; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -224,11 +224,11 @@ static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float
   TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
   TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
   const int mode = d->math_mode;
-  TTS_REQUIRE(mode == tts::MATH_FP32 || mode == tts::MATH_FP32_X6, 1, "unknown math_mode");
+  TTS_REQUIRE(mode >= tts::MATH_FP32 && mode <= tts::MATH_FP32_F16X3, 1, "unknown math_mode");
   if (tile < 0) tile = tts::conv_tile_for(mode, d->Cout, d->K, d->Cin, d->dil, d_res != nullptr);
   const tts::ConvTile t = tts::conv_tile(mode, tile);
   std::vector<float> packed(tts::packed_conv_numel(mode, d->Cout, d->Cin, d->K, t));
-  tts::pack_conv(mode, h_w, d->Cout, d->Cin, d->K, t, packed.data());
+  const int w_exp = tts::pack_conv(mode, h_w, d->Cout, d->Cin, d->K, t, packed.data());
   std::vector<float> bias((size_t)tts::ceil_div(d->Cout, t.BM) * t.BM, 0.f);
   std::memcpy(bias.data(), h_b, sizeof(float) * d->Cout);
   TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
@@ -238,7 +238,16 @@ static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float
   a.dil = d->dil; a.pad = d->dil * (d->K - 1) / 2; a.rep_pad = d->rep_pad;
   a.n_chunks = tts::ceil_div(d->Cin, t.CK);
   a.in_slope = d->in_slope; a.out_slope = d->out_slope; a.zmode = d->zmode; a.zdiv = d->zdiv;
+  a.w_exp = w_exp;
   auto s = static_cast<hipStream_t>(hip_stream);
+  // fp16 hi/lo mode: the input's max-abs statistic (the executors get it from the producer)
+  std::unique_ptr<TmpDev> slots;
+  if (mode == tts::MATH_FP32_F16X3) {
+    slots.reset(new TmpDev(nullptr, (size_t)d->B * 64));
+    TTS_HIP_CHECK(hipMemsetAsync(slots->p, 0, (size_t)d->B * 64 * sizeof(float), s));
+    tts::launch_amax(d_x, (int64_t)d->Cin * d->Tin, d->B, reinterpret_cast<unsigned*>(slots->p), s);
+    a.amax_in = reinterpret_cast<const unsigned*>(slots->p);
+  }
   if (reps <= 0) {
     tts::launch_conv(mode, a, d->B, d->K, tile, s);
   } else {
@@ -271,7 +280,11 @@ int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h
 }
 
 int tts_op_conv1d_num_tiles(int math_mode) {
-  return math_mode == tts::MATH_FP32_X6 ? tts::conv1d_x6_num_tiles() : tts::conv1d_num_tiles();
+  if (math_mode < tts::MATH_FP32 || math_mode > tts::MATH_FP32_F16X3) {
+    g_last_error = "unknown math_mode";
+    return -TTS_ERR_INVALID;
+  }
+  return tts::conv_num_tiles(math_mode);
 }
 
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,

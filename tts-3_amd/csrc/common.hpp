@@ -54,6 +54,10 @@ struct Conv1dArgs {
   float in_slope, out_slope;
   int zmode;
   float zdiv;
+  // MATH_FP32_F16X3 scaling (see kernels_conv_split.hip); ignored by the other modes
+  const unsigned* amax_in;  // [B][64] slots (fp32 bits) whose max bounds |x[b]|, or nullptr (scale 1)
+  unsigned* amax_out;       // [B][64] slots receiving max |stored output[b]|, or nullptr
+  int w_exp;                // packed weights hold w * 2^-w_exp
 };
 
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
@@ -72,6 +76,7 @@ struct ConvTArgs {
   int Cin, Cout, Tin;
   int n_chunks;
   float in_slope;
+  unsigned* amax_out;  // [B][64] slots receiving max |y[b]| (fp32 bits), or nullptr
 };
 
 struct PostArgs {
@@ -96,23 +101,31 @@ void launch_conv_post(const PostArgs& a, int B, hipStream_t s);
 void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
                      int C0, hipStream_t s);
 
-// bf16x6 split-precision conv1d (kernels_conv_x6.hip)
-ConvTile conv1d_x6_tile(int idx);
-int conv1d_x6_num_tiles();
-int conv1d_x6_tile_for(int Cout, int K, int Cin, int dil, bool res);
-void launch_conv1d_x6(const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
-
 // Math modes (TTS_MATH_* in tts_mi355x.h)
-constexpr int MATH_FP32 = 0;     // v_mfma_f32_32x32x2_f32
-constexpr int MATH_FP32_X6 = 1;  // bf16x6 split on v_mfma_f32_32x32x16_bf16
+constexpr int MATH_FP32 = 0;        // v_mfma_f32_32x32x2_f32
+constexpr int MATH_FP32_X6 = 1;     // bf16x6 split on v_mfma_f32_32x32x16_bf16
+constexpr int MATH_FP32_F16X3 = 2;  // scaled fp16 hi/lo split on v_mfma_f32_32x32x16_f16
+
+// Split-precision conv1d (kernels_conv_split.hip), mode MATH_FP32_X6 or MATH_FP32_F16X3.
+ConvTile conv1d_split_tile(int mode, int idx);
+int conv1d_split_num_tiles(int mode);
+int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res);
+void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
+// slots[b][0..63] = max |x[b]| over n floats per item (fp32 bits, atomicMax; zero them first)
+void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s);
 
 // Mode-dispatching helpers used by the executors and the op entry points.
-inline ConvTile conv_tile(int mode, int idx) { return mode == MATH_FP32_X6 ? conv1d_x6_tile(idx) : conv1d_tile(idx); }
-inline int conv_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
-  return mode == MATH_FP32_X6 ? conv1d_x6_tile_for(Cout, K, Cin, dil, res) : conv1d_tile_for(Cout, K, Cin, dil, res);
+inline bool is_split_mode(int mode) { return mode == MATH_FP32_X6 || mode == MATH_FP32_F16X3; }
+inline ConvTile conv_tile(int mode, int idx) {
+  return is_split_mode(mode) ? conv1d_split_tile(mode, idx) : conv1d_tile(idx);
 }
+inline int conv_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
+  return is_split_mode(mode) ? conv1d_split_tile_for(mode, Cout, K, Cin, dil, res)
+                             : conv1d_tile_for(Cout, K, Cin, dil, res);
+}
+inline int conv_num_tiles(int mode) { return is_split_mode(mode) ? conv1d_split_num_tiles(mode) : conv1d_num_tiles(); }
 inline void launch_conv(int mode, const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
-  if (mode == MATH_FP32_X6) launch_conv1d_x6(a, B, K, tile, s);
+  if (is_split_mode(mode)) launch_conv1d_split(mode, a, B, K, tile, s);
   else launch_conv1d(a, B, K, tile, s);
 }
 
@@ -123,14 +136,18 @@ int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] -> [Cout_pad/BM][n_chunks][2U][CK][BM].
 void pack_convT(const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out);
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t);
-void pack_conv1d_x6(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
-int64_t packed_conv1d_x6_numel(int Cout, int Cin, int K, const ConvTile& t);
+// Split modes: [mblock32][cgroup16][K][piece][64][8 x 16-bit] (+2 steps of slack).  Returns the
+// exponent e with which the weights were pre-scaled by 2^-e (0 for bf16x6).
+int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
+int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t);
 inline int64_t packed_conv_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
-  return mode == MATH_FP32_X6 ? packed_conv1d_x6_numel(Cout, Cin, K, t) : packed_conv1d_numel(Cout, Cin, K, t);
+  return is_split_mode(mode) ? packed_conv1d_split_numel(mode, Cout, Cin, K, t) : packed_conv1d_numel(Cout, Cin, K, t);
 }
-inline void pack_conv(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
-  if (mode == MATH_FP32_X6) pack_conv1d_x6(w, Cout, Cin, K, t, out);
-  else pack_conv1d(w, Cout, Cin, K, t, out);
+// returns the weight scale exponent (Conv1dArgs::w_exp)
+inline int pack_conv(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
+  if (is_split_mode(mode)) return pack_conv1d_split(mode, w, Cout, Cin, K, t, out);
+  pack_conv1d(w, Cout, Cin, K, t, out);
+  return 0;
 }
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

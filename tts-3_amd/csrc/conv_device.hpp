@@ -45,7 +45,16 @@ __device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
 // so every value this thread reads is loaded BEFORE its first store: otherwise the compiler
 // cannot hoist a load above the previous element's store and each element pays a full memory
 // round trip (measured: residual convs 2x slower).
-template <int TM, int TN, bool RES, int ZM>
+// Max-abs statistics for the fp16 hi/lo consumers: 64 slots per batch item (slots[b][64]); a
+// wave's max goes to slot blockIdx.x & 63 of its item (fp32 bits order like unsigned integers
+// for non-negative values).  Per item, so an utterance's scaling never depends on its batch.
+__device__ __forceinline__ void publish_amax(unsigned* slots, int b, float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(slots + (size_t)b * 64 + (blockIdx.x & 63), __float_as_uint(v));
+}
+
+template <int TM, int TN, bool RES, int ZM, bool AMAX>
 __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
                                                    int tbase, int cobase, int lane) {
   const int half = lane >> 5;
@@ -64,6 +73,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   const float oslope = a.out_slope;
   const float zdiv = a.zdiv;
   const unsigned rowb = (unsigned)Tout * 4u;
+  float vmax = 0.f;  // AMAX: max |stored value|
   // per 32x32 block: gather every value this thread reads, then compute and store.  Every
   // range-checked offset is in the per-lane voffset (lane row cobase + m*32 + 4*half, column t;
   // register r adds row (r&3) + 8*(r>>2)); an absent cvec reads 0 through a 0-byte descriptor.
@@ -90,6 +100,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
         if (RES) rv[r] = bload(rres, vo[r], 0u);
         if (ZM >= 2) zv[r] = bload(rz, vo[r], 0u);
       }
+      float vm = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float v = (acc[m][n][r] + bv[r]) * mv;  // mv = 1 without a mask (exact)
@@ -97,28 +108,31 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
         if (RES) v += rv[r];
         if (ZM == 2) v = zv[r] + v;
         if (ZM == 3) v = (zv[r] + v) / zdiv;
+        if (AMAX) vm = fmaxf(vm, fabsf(v));  // rows >= Cout hold exact zeros
         bstore(rout, v, vo[r], 0u);
       }
+      if (AMAX && t < Tout) vmax = fmaxf(vmax, vm);
     }
   }
+  if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
 }
 
 // The per-element options are template parameters (one uniform dispatch per tile), so the
 // unrolled epilogue carries no per-element branches.
-template <int TM, int TN>
+template <int TM, int TN, bool AMAX = false>
 __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
                                               int tbase, int cobase, int lane) {
   // copy the argument block: a store through `out` could alias it in the compiler's view
   const Conv1dArgs a = args;
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
   if (a.res) {
-    if (zm == 0) conv_epilogue_impl<TM, TN, true, 0>(a, acc, b, tbase, cobase, lane);
-    else if (zm == 2) conv_epilogue_impl<TM, TN, true, 2>(a, acc, b, tbase, cobase, lane);
-    else conv_epilogue_impl<TM, TN, true, 3>(a, acc, b, tbase, cobase, lane);
+    if (zm == 0) conv_epilogue_impl<TM, TN, true, 0, AMAX>(a, acc, b, tbase, cobase, lane);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, true, 2, AMAX>(a, acc, b, tbase, cobase, lane);
+    else conv_epilogue_impl<TM, TN, true, 3, AMAX>(a, acc, b, tbase, cobase, lane);
   } else {
-    if (zm == 0) conv_epilogue_impl<TM, TN, false, 0>(a, acc, b, tbase, cobase, lane);
-    else if (zm == 2) conv_epilogue_impl<TM, TN, false, 2>(a, acc, b, tbase, cobase, lane);
-    else conv_epilogue_impl<TM, TN, false, 3>(a, acc, b, tbase, cobase, lane);
+    if (zm == 0) conv_epilogue_impl<TM, TN, false, 0, AMAX>(a, acc, b, tbase, cobase, lane);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, false, 2, AMAX>(a, acc, b, tbase, cobase, lane);
+    else conv_epilogue_impl<TM, TN, false, 3, AMAX>(a, acc, b, tbase, cobase, lane);
   }
 }
 

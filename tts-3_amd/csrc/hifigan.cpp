@@ -77,7 +77,7 @@ void hifigan_validate(const TtsHifiganCfg& c) {
   }
   TTS_REQUIRE(c.inference_padding >= 0, 1, "inference_padding must be >= 0");
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
-  TTS_REQUIRE(c.math_mode == MATH_FP32 || c.math_mode == MATH_FP32_X6, 1, "unknown math_mode");
+  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_FP32_F16X3, 1, "unknown math_mode");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -94,19 +94,22 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const int mode = cfg_.math_mode;
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
-  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res) {
+  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
     ConvLayer L;
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
-    L.tile = conv_tile_for(mode, Cout, K, Cin, dil, res);
-    const ConvTile t = conv_tile(mode, L.tile);
+    L.mode = lmode;
+    L.tile = conv_tile_for(lmode, Cout, K, Cin, dil, res);
+    const ConvTile t = conv_tile(lmode, L.tile);
     L.n_chunks = ceil_div(Cin, t.CK);
-    L.w_numel = packed_conv_numel(mode, Cout, Cin, K, t);
+    L.w_numel = packed_conv_numel(lmode, Cout, Cin, K, t);
     L.b_numel = (int64_t)ceil_div(Cout, t.BM) * t.BM;
     L.name = std::string(fam) + "_k" + std::to_string(K) + "_c" + std::to_string(Cout);
     return L;
   };
 
-  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre", false);
+  // conv_pre reads the caller's mel, which carries no max-abs statistics: bf16x6 in the fp16
+  // hi/lo mode (0.6% of the FLOPs)
+  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre", false, mode == MATH_FP32_F16X3 ? MATH_FP32_X6 : mode);
   src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
     ConvTLayer L;
@@ -133,14 +136,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         for (int m = 0; m < 3; ++m) { w1[m] = hw[wi]; b1[m] = hw[wi + 1]; wi += 2; }
         for (int m = 0; m < 3; ++m) { w2[m] = hw[wi]; b2[m] = hw[wi + 1]; wi += 2; }
         for (int m = 0; m < 3; ++m) {
-          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false));
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false, mode));
           src.push_back({w1[m], b1[m]});
-          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true));
+          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true, mode));
           src.push_back({w2[m], b2[m]});
         }
       } else {
         for (int m = 0; m < 2; ++m) {
-          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", true));
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", true, mode));
           src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
         }
       }
@@ -174,8 +177,8 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     // src[0] is conv_pre; src[1..] resblocks
     size_t si = 0;
     for (auto* c : convs) {
-      const ConvTile t = conv_tile(mode, c->tile);
-      pack_conv(mode, src[si].first, c->Cout, c->Cin, c->K, t, host.data() + off);
+      const ConvTile t = conv_tile(c->mode, c->tile);
+      c->w_exp = pack_conv(c->mode, src[si].first, c->Cout, c->Cin, c->K, t, host.data() + off);
       offs.push_back(off); off += align(c->w_numel);
       std::memcpy(host.data() + off, src[si].second, sizeof(float) * c->Cout);
       offs.push_back(off); off += align(c->b_numel);
@@ -233,9 +236,14 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
   return ((best * B + 63) / 64) * 64;
 }
 
+// max-abs slot groups (fp16 hi/lo mode), [B][64] each: per stage the upsampled input o, then
+// per resblock conv its output (convs1 -> t, convs2 -> x)
+int Hifigan::amax_groups() const { return cfg_.num_upsamples * (1 + cfg_.num_kernels * 6); }
+
 int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
   const int64_t cond = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
-  return (4 * plane_floats(B, T, pad) + cond) * (int64_t)sizeof(float);
+  const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
+  return (4 * plane_floats(B, T, pad) + cond + amax) * (int64_t)sizeof(float);
 }
 
 void Hifigan::reserve(int B, int T, int pad) {
@@ -265,6 +273,11 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   float* bufX = ws_ + 2 * plane;  // resblock running residual x
   float* bufT = ws_ + 3 * plane;  // convs1 output (already leaky-relu'd)
   float* cvec = cfg_.cond_channels > 0 ? ws_ + 4 * plane : nullptr;
+  const int64_t cond_floats = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
+  const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + 4 * plane + cond_floats) : nullptr;
+  auto slots = [&](int grp) -> unsigned* { return amax ? amax + (size_t)grp * B * 64 : nullptr; };  // [B][64]
+  if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, (size_t)amax_groups() * B * 64 * sizeof(unsigned), s));
 
   const int L = T + 2 * pad;
   const int C0 = cfg_.upsample_initial_channel;
@@ -274,8 +287,10 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   }
 
   auto conv = [&](const ConvLayer& Ld, const float* x, int Tin, int Tout, int rep, float in_slope,
-                  float out_slope, const float* res, float* y, int zmode, const float* cv) {
+                  float out_slope, const float* res, float* y, int zmode, const float* cv,
+                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
     Conv1dArgs a{};
+    a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = Ld.w_exp;
     a.x = x; a.w = Ld.w; a.bias = Ld.b; a.res = res; a.y = y; a.z = bufZ; a.cvec = cv;
     a.Cin = Ld.Cin; a.Cout = Ld.Cout; a.Tin = Tin; a.Tout = Tout;
     a.dil = Ld.dil; a.pad = Ld.pad; a.rep_pad = rep; a.n_chunks = Ld.n_chunks;
@@ -284,7 +299,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     double bytes = 4.0 * ((double)B * Ld.Cin * Tin + (double)Ld.Cout * Ld.Cin * Ld.K + (double)B * Ld.Cout * Tout);
     if (res) bytes += 4.0 * B * Ld.Cout * (double)Tout;
     if (zmode >= 2) bytes += 4.0 * B * Ld.Cout * (double)Tout;
-    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv(cfg_.math_mode, a, B, Ld.K, Ld.tile, s); });
+    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv(Ld.mode, a, B, Ld.K, Ld.tile, s); });
   };
 
   // conv_pre on the replicate-padded mel (hifigan_generator.py:281, :249) [+ cond_layer(g), :250-251]
@@ -297,6 +312,8 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     ConvTArgs ta{};
     ta.x = cur; ta.w = U.w; ta.bias = U.b; ta.y = bufO;
     ta.Cin = U.Cin; ta.Cout = U.Cout; ta.Tin = len; ta.n_chunks = U.n_chunks; ta.in_slope = 0.1f;
+    const int g0 = i * (1 + cfg_.num_kernels * 6);  // this stage's slot groups: o, then per conv
+    ta.amax_out = slots(g0);
     const int lout = len * U.U;
     run(prof, s, U.name.c_str(), 2.0 * B * U.Cout * (double)U.Cin * 2 * lout,
         4.0 * ((double)B * U.Cin * len + (double)U.Cin * U.Cout * 2 * U.U + (double)B * U.Cout * lout),
@@ -306,21 +323,26 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     for (int j = 0; j < cfg_.num_kernels; ++j) {
       const ResBlock& rb = res_[i * cfg_.num_kernels + j];
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
+      const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
       if (cfg_.resblock_type == 1) {
         for (int m = 0; m < 3; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;
-          // xt = convs1[m](lrelu(x)); xt = lrelu(xt)       (ResBlock1.forward :94-96)
-          conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr);
-          // x = convs2[m](xt) + x                          (:97-98)
+          const unsigned* xin_amax = (m == 0) ? slots(g0) : slots(gj + 2 * m - 1);
           const bool last = (m == 2);
-          conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr);
+          // xt = convs1[m](lrelu(x)); xt = lrelu(xt)       (ResBlock1.forward :94-96)
+          conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr, xin_amax, slots(gj + 2 * m));
+          // x = convs2[m](xt) + x                          (:97-98)
+          conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr,
+               slots(gj + 2 * m), last ? nullptr : slots(gj + 2 * m + 1));
         }
       } else {
         for (int m = 0; m < 2; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;
+          const unsigned* xin_amax = (m == 0) ? slots(g0) : slots(gj + m - 1);
           const bool last = (m == 1);
           // x = convs[m](lrelu(x)) + x                     (ResBlock2.forward :151-154)
-          conv(rb.convs[m], xin, len, len, 0, 0.1f, 1.f, xin, bufX, last ? zlast : 0, nullptr);
+          conv(rb.convs[m], xin, len, len, 0, 0.1f, 1.f, xin, bufX, last ? zlast : 0, nullptr, xin_amax,
+               last ? nullptr : slots(gj + m));
         }
       }
     }

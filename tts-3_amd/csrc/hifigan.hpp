@@ -74,6 +74,8 @@ class Hifigan {
  private:
   struct ConvLayer {
     int Cin = 0, Cout = 0, K = 0, dil = 1, pad = 0, tile = 0, n_chunks = 0;
+    int mode = 0;   // math mode of this layer (TTS_MATH_*)
+    int w_exp = 0;  // packed weights hold w * 2^-w_exp (fp16 hi/lo mode)
     int64_t w_numel = 0, b_numel = 0;
     float* w = nullptr;
     float* b = nullptr;
@@ -91,6 +93,7 @@ class Hifigan {
   };
 
   int64_t plane_floats(int B, int T, int pad) const;
+  int amax_groups() const;
 
   TtsHifiganCfg cfg_;
   int device_;

@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
 
   const int Cout = a.Cout;
   constexpr int P = U / 2;
+  float vmax = 0.f;  // max |stored value| for the fp16 hi/lo consumers (amax_out)
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
 #pragma unroll
@@ -358,23 +359,30 @@ __global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
           if (mm >= 1) {
             f32x4 v = {acc[0][m][n][r] + bb, acc[1][m][n][r] + bb, acc[2][m][n][r] + bb,
                        acc[3][m][n][r] + bb};
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             *reinterpret_cast<f32x4*>(yrow + 8 * mm - 4) = v;
           }
           if (mm < Tin) {
             f32x4 v = {acc[4][m][n][r] + bb, acc[5][m][n][r] + bb, acc[6][m][n][r] + bb,
                        acc[7][m][n][r] + bb};
+            vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             *reinterpret_cast<f32x4*>(yrow + 8 * mm) = v;
           }
         } else {
 #pragma unroll
           for (int s = 0; s < U; ++s) {
             const int t = U * mm + s - P;
-            if (t >= 0 && t < Tout) yrow[t] = acc[s][m][n][r] + bb;
+            if (t >= 0 && t < Tout) {
+              const float v = acc[s][m][n][r] + bb;
+              vmax = fmaxf(vmax, fabsf(v));
+              yrow[t] = v;
+            }
           }
         }
       }
     }
   }
+  if (a.amax_out) publish_amax(a.amax_out, b, vmax);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -531,6 +539,9 @@ ConvTile conv1d_tile(int idx) {
 int conv1d_num_tiles() { return kNumConvTiles; }
 
 void launch_conv1d(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
+  TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
+              "conv1d: a batch item's channel plane exceeds 2 GiB");
   switch (K) {
     case 1: launch_conv1d_k<1>(a, B, tile, s); break;
     case 3: launch_conv1d_k<3>(a, B, tile, s); break;

@@ -1,5 +1,7 @@
 // Host-side packing of PyTorch conv weights into the chunked layouts the MFMA kernels
 // stage into LDS with contiguous 16-byte loads.
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 
 #include "common.hpp"
@@ -54,16 +56,39 @@ void split3_host(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
   p2 = f2bf_rne(r2);
 }
 
-// bf16x6 A-operand fragments (conv1d_x6_kernel), in floats (2 bf16 per float):
-//   out[mb][c16][k][piece][lane][j] = piece_p(w[mb*32 + (lane&31)][c16*16 + 8*(lane>>5) + j][k])
-// plus 2 steps of slack for the prefetch.
-int64_t packed_conv1d_x6_numel(int Cout, int Cin, int K, const ConvTile& t) {
-  const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
-  const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 16);
-  return (mblocks * groups * K + 2) * 3 * 64 * 4;
+// fp16 hi/lo split of a value already scaled into [0, 2^14] magnitude: x ~ hi + lo
+// (round-to-nearest-even, as the device's v_cvt_f16_f32; see kernels_conv_split.hip).
+static inline void split_h3_host(float x, uint16_t& hi, uint16_t& lo) {
+  const _Float16 h = (_Float16)x;
+  hi = __builtin_bit_cast(uint16_t, h);
+  lo = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)h));
 }
 
-void pack_conv1d_x6(const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f) {
+static int split_pieces(int mode) { return mode == MATH_FP32_F16X3 ? 2 : 3; }
+
+// Split-mode A-operand fragments (conv1d_split_kernel), in floats (2 x 16-bit per float):
+//   out[mb][c16][k][piece][lane][j] = piece_p(w'[mb*32 + (lane&31)][c16*16 + 8*(lane>>5) + j][k])
+// plus 2 steps of slack for the prefetch.  w' = w for bf16x6, w * 2^-e for fp16 hi/lo with e
+// chosen so max|w'| lies in [2^13, 2^14) (exact; undone in the kernel epilogue).
+int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
+  const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
+  const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 16);
+  return (mblocks * groups * K + 2) * split_pieces(mode) * 64 * 4;
+}
+
+int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f) {
+  const int NP = split_pieces(mode);
+  int e = 0;
+  if (mode == MATH_FP32_F16X3) {
+    float m = 0.f;
+    for (int64_t i = 0; i < (int64_t)Cout * Cin * K; ++i) m = std::max(m, std::fabs(w[i]));
+    TTS_REQUIRE(std::isfinite(m), 1, "conv weights contain inf/NaN");
+    if (m > 0.f) {
+      int E;
+      (void)std::frexp(m, &E);
+      e = E - 14;
+    }
+  }
   uint16_t* out = reinterpret_cast<uint16_t*>(out_f);
   const int mblocks = ceil_div(Cout, t.BM) * (t.BM / 32);
   const int groups = ceil_div(Cin, t.CK) * (t.CK / 16);
@@ -77,13 +102,15 @@ void pack_conv1d_x6(const float* w, int Cout, int Cin, int K, const ConvTile& t,
             const int co = mb * 32 + (lane & 31);
             const int ci = c16 * 16 + 8 * (lane >> 5) + j;
             const float v = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
-            split3_host(v, pc[0][lane][j], pc[1][lane][j], pc[2][lane][j]);
+            if (NP == 3) split3_host(v, pc[0][lane][j], pc[1][lane][j], pc[2][lane][j]);
+            else split_h3_host(std::ldexp(v, -e), pc[0][lane][j], pc[1][lane][j]);
           }
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           for (int lane = 0; lane < 64; ++lane)
             for (int j = 0; j < 8; ++j) out[o++] = pc[p][lane][j];
       }
-  for (int i = 0; i < 2 * 3 * 64 * 8; ++i) out[o++] = 0;
+  for (int i = 0; i < 2 * NP * 64 * 8; ++i) out[o++] = 0;
+  return e;
 }
 
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t) {
