@@ -212,10 +212,11 @@ int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h
 int tts_op_conv1d_num_tiles(int math_mode);
 
 /* y = conv_transpose1d(act_in(x), w[Cin][Cout][K], b, stride, padding=(K-stride)/2);
- * requires K == 2*stride (every HiFiGAN config). */
+ * requires K == 2*stride (every HiFiGAN config) with stride 2, 4 or 8; math_mode TTS_MATH_*
+ * (the split modes run the polyphase K=2 conv form of the executor). */
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
                             const float* h_b, int Cout, int K, int stride, float in_slope,
-                            float* d_y, void* hip_stream);
+                            int math_mode, float* d_y, void* hip_stream);
 
 /* y[B][1][T] = tanh(conv1d(leaky_relu(z, in_slope), w[1][Cin][7], b, pad 3)). */
 int tts_op_conv_post(const float* d_z, int B, int Cin, int T, const float* h_w, const float* h_b,

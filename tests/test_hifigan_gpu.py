@@ -96,8 +96,9 @@ CONVT_CASES = [
 ]
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("case", CONVT_CASES, ids=[f"t{i}" for i in range(len(CONVT_CASES))])
-def test_op_conv_transpose1d(cuda_device, case):
+def test_op_conv_transpose1d(cuda_device, case, mode):
     B, Cin, Cout, T, U = case
     K = 2 * U
     g = _rng(1000 + T)
@@ -108,7 +109,7 @@ def test_op_conv_transpose1d(cuda_device, case):
     y = torch.full((B, Cout, U * T), float("nan"), device=cuda_device)
     wn, bn = w.numpy().copy(), b.numpy().copy()
     N.call("tts_op_conv_transpose1d", N.ptr(x.to(cuda_device)), B, Cin, T, N.ptr(wn), N.ptr(bn), Cout, K, U, 0.1,
-           N.ptr(y), N.stream_ptr(cuda_device))
+           N.MATH_MODES[mode], N.ptr(y), N.stream_ptr(cuda_device))
     assert_close_fp32(y.cpu(), ref, f"convT {case}")
 
 

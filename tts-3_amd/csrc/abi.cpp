@@ -66,7 +66,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 102; }
+int tts_abi_version(void) { return 103; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -289,11 +289,39 @@ int tts_op_conv1d_num_tiles(int math_mode) {
 
 int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const float* h_w,
                             const float* h_b, int Cout, int K, int stride, float in_slope,
-                            float* d_y, void* hip_stream) {
+                            int math_mode, float* d_y, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(d_x && h_w && h_b && d_y, 1, "NULL argument");
     TTS_REQUIRE(B >= 1 && Cin >= 1 && Cout >= 1 && Tin >= 1, 1, "bad conv_transpose1d shape");
     TTS_REQUIRE(K == 2 * stride, 3, "conv_transpose1d: requires kernel_size == 2*stride");
+    TTS_REQUIRE(stride == 2 || stride == 4 || stride == 8, 3, "conv_transpose1d: stride must be 2, 4 or 8");
+    TTS_REQUIRE(math_mode >= tts::MATH_FP32 && math_mode <= tts::MATH_FP32_F16X3, 1, "unknown math_mode");
+    auto s = static_cast<hipStream_t>(hip_stream);
+    if (tts::is_split_mode(math_mode)) {
+      const int tile = tts::conv_tile_for(math_mode, stride * Cout, 2, Cin, 1, false);
+      const tts::ConvTile t = tts::conv_tile(math_mode, tile);
+      std::vector<float> packed(tts::packed_conv_numel(math_mode, stride * Cout, Cin, 2, t));
+      const int w_exp = tts::pack_convT_split(math_mode, h_w, Cin, Cout, stride, t, packed.data());
+      std::vector<float> bias((size_t)tts::ceil_div(stride * Cout, t.BM) * t.BM, 0.f);
+      for (int co = 0; co < Cout; ++co)
+        for (int ph = 0; ph < stride; ++ph) bias[(size_t)co * stride + ph] = h_b[co];
+      TmpDev w(packed.data(), packed.size()), b(bias.data(), bias.size());
+      tts::Conv1dArgs a{};
+      a.x = d_x; a.w = w.p; a.bias = b.p; a.y = d_y;
+      a.Cin = Cin; a.Cout = stride * Cout; a.Tin = Tin; a.Tout = Tin + 1;
+      a.dil = 1; a.pad = 1; a.n_chunks = tts::ceil_div(Cin, t.CK);
+      a.in_slope = in_slope; a.out_slope = 1.f; a.zdiv = 1.f; a.w_exp = w_exp; a.ups = stride;
+      std::unique_ptr<TmpDev> slots;
+      if (math_mode == tts::MATH_FP32_F16X3) {
+        slots.reset(new TmpDev(nullptr, (size_t)B * 64));
+        TTS_HIP_CHECK(hipMemsetAsync(slots->p, 0, (size_t)B * 64 * sizeof(float), s));
+        tts::launch_amax(d_x, (int64_t)Cin * Tin, B, reinterpret_cast<unsigned*>(slots->p), s);
+        a.amax_in = reinterpret_cast<const unsigned*>(slots->p);
+      }
+      tts::launch_conv(math_mode, a, B, 2, tile, s);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+      return;
+    }
     const int tile = tts::convT_tile_for(Cout, stride);
     const tts::ConvTile t = tts::convT_tile(tile, stride);
     std::vector<float> packed(tts::packed_convT_numel(Cin, Cout, stride, t));
@@ -304,7 +332,6 @@ int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const flo
     tts::ConvTArgs a{};
     a.x = d_x; a.w = w.p; a.bias = b.p; a.y = d_y;
     a.Cin = Cin; a.Cout = Cout; a.Tin = Tin; a.n_chunks = tts::ceil_div(Cin, t.CK); a.in_slope = in_slope;
-    auto s = static_cast<hipStream_t>(hip_stream);
     tts::launch_convT(a, B, stride, tile, s);
     TTS_HIP_CHECK(hipStreamSynchronize(s));
   });

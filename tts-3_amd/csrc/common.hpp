@@ -58,6 +58,11 @@ struct Conv1dArgs {
   const unsigned* amax_in;  // [B][64] slots (fp32 bits) whose max bounds |x[b]|, or nullptr (scale 1)
   unsigned* amax_out;       // [B][64] slots receiving max |stored output[b]|, or nullptr
   int w_exp;                // packed weights hold w * 2^-w_exp
+  // ups = U > 0 (split kernels, K = 2): polyphase ConvTranspose1d(kernel 2U, stride U, padding
+  // U/2).  Rows are rho = co*U + s (Cout = U * channels), columns are frames m in [0, Tin]
+  // (Tout = Tin + 1, pad = 1: taps x[m-1], x[m]); row rho, column m is stored at time
+  // U*m + s - U/2 of y[b][co][0 .. U*Tin).  zmode 0, no res / mask / cvec.
+  int ups;
 };
 
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
@@ -140,6 +145,9 @@ int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t);
 // exponent e with which the weights were pre-scaled by 2^-e (0 for bf16x6).
 int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
 int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t);
+// ConvTranspose1d torch weight [Cin][Cout][2U] as the K=2 conv of Conv1dArgs::ups (U*Cout rows);
+// returns w_exp.  Its bias is the conv's bias repeated per phase: bias'[co*U + s] = bias[co].
+int pack_convT_split(int mode, const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out);
 inline int64_t packed_conv_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
   return is_split_mode(mode) ? packed_conv1d_split_numel(mode, Cout, Cin, K, t) : packed_conv1d_numel(Cout, Cin, K, t);
 }

@@ -117,6 +117,50 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
 }
 
+// Polyphase ConvTranspose1d epilogue (Conv1dArgs::ups = U): row rho = co*U + s, column frame m
+// -> y[b][co][U*m + s - U/2].  For U = 8 a lane's registers r = 4i..4i+3 hold the phases
+// 4*half .. 4*half+3 of one channel, i.e. 4 consecutive samples.
+template <int TM, int TN, bool AMAX>
+__device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b, int tbase,
+                                               int cobase, int lane) {
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int U = a.ups;
+  const int lgU = __builtin_ctz(U);
+  const int Cr = a.Cout >> lgU;   // channels
+  const int Tin = a.Tin;
+  const int To = Tin << lgU;      // output samples
+  const unsigned plane = (unsigned)Cr * (unsigned)To * 4u;
+  const rsrc_t rout = make_rsrc(a.y + (size_t)b * Cr * To, plane);
+  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)a.Cout * 4u);
+  float vmax = 0.f;
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned rho = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
+      bv[r] = bload(rbias, rho * 4u, 0u);
+    }
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int mm = tbase + n * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rho = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const int co = rho >> lgU;
+        const int t = (mm << lgU) + (rho & (U - 1)) - (U >> 1);
+        // rows >= Cout land past the plane (co >= Cr); samples outside [0, To) are marked OOB
+        const unsigned off = (t >= 0 && t < To) ? ((unsigned)co * (unsigned)To + (unsigned)t) * 4u : OOB_OFF;
+        const float v = acc[m][n][r] + bv[r];
+        if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v));
+        bstore(rout, v, off, 0u);
+      }
+    }
+  }
+  if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
+}
+
 // The per-element options are template parameters (one uniform dispatch per tile), so the
 // unrolled epilogue carries no per-element branches.
 template <int TM, int TN, bool AMAX = false>

@@ -107,18 +107,26 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     return L;
   };
 
-  // conv_pre reads the caller's mel, which carries no max-abs statistics: bf16x6 in the fp16
-  // hi/lo mode (0.6% of the FLOPs)
-  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre", false, mode == MATH_FP32_F16X3 ? MATH_FP32_X6 : mode);
+  pre_ = add_conv(cfg_.in_channels, C0, 7, 1, "conv_pre", false, mode);
   src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
     ConvTLayer L;
     L.Cin = C0 >> i; L.Cout = C0 >> (i + 1); L.U = cfg_.upsample_factors[i];
-    L.tile = convT_tile_for(L.Cout, L.U);
-    const ConvTile t = convT_tile(L.tile, L.U);
-    L.n_chunks = ceil_div(L.Cin, t.CK);
-    L.w_numel = packed_convT_numel(L.Cin, L.Cout, L.U, t);
-    L.b_numel = (int64_t)ceil_div(L.Cout, t.BM) * t.BM;
+    L.mode = mode;
+    if (is_split_mode(mode)) {
+      // split modes: the K=2 polyphase conv form (Conv1dArgs::ups), U*Cout rows
+      L.tile = conv_tile_for(mode, L.U * L.Cout, 2, L.Cin, 1, false);
+      const ConvTile t = conv_tile(mode, L.tile);
+      L.n_chunks = ceil_div(L.Cin, t.CK);
+      L.w_numel = packed_conv_numel(mode, L.U * L.Cout, L.Cin, 2, t);
+      L.b_numel = (int64_t)ceil_div(L.U * L.Cout, t.BM) * t.BM;
+    } else {
+      L.tile = convT_tile_for(L.Cout, L.U);
+      const ConvTile t = convT_tile(L.tile, L.U);
+      L.n_chunks = ceil_div(L.Cin, t.CK);
+      L.w_numel = packed_convT_numel(L.Cin, L.Cout, L.U, t);
+      L.b_numel = (int64_t)ceil_div(L.Cout, t.BM) * t.BM;
+    }
     L.name = "ups_u" + std::to_string(L.U) + "_c" + std::to_string(L.Cout);
     ups_.push_back(L);
   }
@@ -187,10 +195,18 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   }
   for (size_t i = 0; i < ups_.size(); ++i) {
     auto& u = ups_[i];
-    const ConvTile t = convT_tile(u.tile, u.U);
-    pack_convT(usrc[i].first, u.Cin, u.Cout, u.U, t, host.data() + off);
-    offs.push_back(off); off += align(u.w_numel);
-    std::memcpy(host.data() + off, usrc[i].second, sizeof(float) * u.Cout);
+    if (is_split_mode(u.mode)) {
+      const ConvTile t = conv_tile(u.mode, u.tile);
+      u.w_exp = pack_convT_split(u.mode, usrc[i].first, u.Cin, u.Cout, u.U, t, host.data() + off);
+      offs.push_back(off); off += align(u.w_numel);
+      for (int co = 0; co < u.Cout; ++co)
+        for (int ph = 0; ph < u.U; ++ph) host[off + (int64_t)co * u.U + ph] = usrc[i].second[co];
+    } else {
+      const ConvTile t = convT_tile(u.tile, u.U);
+      pack_convT(usrc[i].first, u.Cin, u.Cout, u.U, t, host.data() + off);
+      offs.push_back(off); off += align(u.w_numel);
+      std::memcpy(host.data() + off, usrc[i].second, sizeof(float) * u.Cout);
+    }
     offs.push_back(off); off += align(u.b_numel);
   }
   std::memcpy(host.data() + off, post_w_, sizeof(float) * Cl * 7);
@@ -236,9 +252,11 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
   return ((best * B + 63) / 64) * 64;
 }
 
-// max-abs slot groups (fp16 hi/lo mode), [B][64] each: per stage the upsampled input o, then
-// per resblock conv its output (convs1 -> t, convs2 -> x)
-int Hifigan::amax_groups() const { return cfg_.num_upsamples * (1 + cfg_.num_kernels * 6); }
+// max-abs slot groups (fp16 hi/lo mode), [B][64] each: 0 the mel, 1 conv_pre's output, then per
+// stage i from stage_group(i): the upsampled input o, per resblock conv its output
+// (convs1 -> t, convs2 -> x), and the stage's MRF output z/num_kernels
+int Hifigan::amax_groups() const { return 2 + cfg_.num_upsamples * (2 + cfg_.num_kernels * 6); }
+int Hifigan::stage_group(int i) const { return 2 + i * (2 + cfg_.num_kernels * 6); }
 
 int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
   const int64_t cond = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
@@ -303,27 +321,41 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   };
 
   // conv_pre on the replicate-padded mel (hifigan_generator.py:281, :249) [+ cond_layer(g), :250-251]
-  conv(pre_, mel, T, L, pad, 1.f, 1.f, nullptr, bufZ, 0, cvec);
+  if (h3)
+    run(prof, s, "amax_mel", 0.0, 4.0 * B * C * (double)T,
+        [&] { launch_amax(mel, (int64_t)C * T, B, slots(0), s); });
+  conv(pre_, mel, T, L, pad, 1.f, 1.f, nullptr, bufZ, 0, cvec, slots(0), slots(1));
 
   int len = L;
   const float* cur = bufZ;
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
     const ConvTLayer& U = ups_[i];
-    ConvTArgs ta{};
-    ta.x = cur; ta.w = U.w; ta.bias = U.b; ta.y = bufO;
-    ta.Cin = U.Cin; ta.Cout = U.Cout; ta.Tin = len; ta.n_chunks = U.n_chunks; ta.in_slope = 0.1f;
-    const int g0 = i * (1 + cfg_.num_kernels * 6);  // this stage's slot groups: o, then per conv
-    ta.amax_out = slots(g0);
+    const int g0 = stage_group(i);  // this stage's slot groups: o, per conv, z
+    const unsigned* z_amax = slots(i == 0 ? 1 : stage_group(i - 1) + 1 + cfg_.num_kernels * 6);
     const int lout = len * U.U;
-    run(prof, s, U.name.c_str(), 2.0 * B * U.Cout * (double)U.Cin * 2 * lout,
-        4.0 * ((double)B * U.Cin * len + (double)U.Cin * U.Cout * 2 * U.U + (double)B * U.Cout * lout),
-        [&] { launch_convT(ta, B, U.U, U.tile, s); });
+    const double uflops = 2.0 * B * U.Cout * (double)U.Cin * 2 * lout;
+    const double ubytes = 4.0 * ((double)B * U.Cin * len + (double)U.Cin * U.Cout * 2 * U.U + (double)B * U.Cout * lout);
+    if (is_split_mode(U.mode)) {
+      Conv1dArgs a{};
+      a.x = cur; a.w = U.w; a.bias = U.b; a.y = bufO;
+      a.Cin = U.Cin; a.Cout = U.U * U.Cout; a.Tin = len; a.Tout = len + 1;
+      a.dil = 1; a.pad = 1; a.n_chunks = U.n_chunks;
+      a.in_slope = 0.1f; a.out_slope = 1.f; a.zdiv = 1.f;
+      a.amax_in = z_amax; a.amax_out = slots(g0); a.w_exp = U.w_exp; a.ups = U.U;
+      run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_conv(U.mode, a, B, 2, U.tile, s); });
+    } else {
+      ConvTArgs ta{};
+      ta.x = cur; ta.w = U.w; ta.bias = U.b; ta.y = bufO;
+      ta.Cin = U.Cin; ta.Cout = U.Cout; ta.Tin = len; ta.n_chunks = U.n_chunks; ta.in_slope = 0.1f;
+      run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_convT(ta, B, U.U, U.tile, s); });
+    }
     len = lout;
     // MRF: z = sum_j resblock_j(o); o = z / num_kernels (:255-261)
     for (int j = 0; j < cfg_.num_kernels; ++j) {
       const ResBlock& rb = res_[i * cfg_.num_kernels + j];
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
       const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
+      const int gz = g0 + 1 + cfg_.num_kernels * 6;  // the stage's z / num_kernels
       if (cfg_.resblock_type == 1) {
         for (int m = 0; m < 3; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;
@@ -333,7 +365,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
           conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr, xin_amax, slots(gj + 2 * m));
           // x = convs2[m](xt) + x                          (:97-98)
           conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr,
-               slots(gj + 2 * m), last ? nullptr : slots(gj + 2 * m + 1));
+               slots(gj + 2 * m), last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1));
         }
       } else {
         for (int m = 0; m < 2; ++m) {
@@ -342,7 +374,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
           const bool last = (m == 1);
           // x = convs[m](lrelu(x)) + x                     (ResBlock2.forward :151-154)
           conv(rb.convs[m], xin, len, len, 0, 0.1f, 1.f, xin, bufX, last ? zlast : 0, nullptr, xin_amax,
-               last ? nullptr : slots(gj + m));
+               last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + m));
         }
       }
     }

@@ -83,6 +83,8 @@ class Hifigan {
   };
   struct ConvTLayer {
     int Cin = 0, Cout = 0, U = 0, tile = 0, n_chunks = 0;
+    int mode = 0;   // split modes run the K=2 polyphase conv form (Conv1dArgs::ups)
+    int w_exp = 0;
     int64_t w_numel = 0, b_numel = 0;
     float* w = nullptr;
     float* b = nullptr;
@@ -94,6 +96,7 @@ class Hifigan {
 
   int64_t plane_floats(int B, int T, int pad) const;
   int amax_groups() const;
+  int stage_group(int i) const;
 
   TtsHifiganCfg cfg_;
   int device_;

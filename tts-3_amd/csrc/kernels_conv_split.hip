@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     const int g = rr / XW;
     const int r = rr - g * XW;
     const int ts = t0 - a.pad + r;
-    const bool ok = (g < G) && ts >= 0 && ts < Tout;
+    // source frame ts - rep_pad, clamped (replicate) when rep_pad > 0, else zero outside [0, Tin)
+    const bool ok = (g < G) && ts >= 0 && ts < (a.rep_pad ? Tout : Tin);
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
     uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
@@ -293,7 +294,11 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
 #pragma unroll
       for (int n = 0; n < TN; ++n) acc[0][m][n] *= sc;
   }
-  conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+  if constexpr (K == 2) {
+    convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+  } else {
+    conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+  }
 }
 
 // slots[b][blockIdx.x & 63] = max |x[b]| (grid-stride per item), for inputs without producer
@@ -374,6 +379,7 @@ template <class S>
 void launch_split_s(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
   switch (K) {
     case 1: launch_split_k<S, 1>(a, B, tile, s); break;
+    case 2: launch_split_k<S, 2>(a, B, tile, s); break;  // ConvTranspose1d (Conv1dArgs::ups)
     case 3: launch_split_k<S, 3>(a, B, tile, s); break;
     case 5: launch_split_k<S, 5>(a, B, tile, s); break;
     case 7: launch_split_k<S, 7>(a, B, tile, s); break;
@@ -410,6 +416,10 @@ int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res)
 }
 
 void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  TTS_REQUIRE((K == 2) == (a.ups > 0), 1, "conv1d(split): K == 2 is the ConvTranspose1d form (ups > 0)");
+  TTS_REQUIRE(a.ups == 0 || ((a.ups & (a.ups - 1)) == 0 && a.Cout % a.ups == 0 && a.zmode == 0 && !a.res &&
+                             !a.mask && !a.cvec && a.Tout == a.Tin + 1 && a.pad == 1),
+              1, "conv1d(split): bad ConvTranspose1d arguments");
   // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "common.hpp"
 
@@ -111,6 +112,22 @@ int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const 
       }
   for (int i = 0; i < 2 * NP * 64 * 8; ++i) out[o++] = 0;
   return e;
+}
+
+int pack_convT_split(int mode, const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out) {
+  // y[co][U*m + s - U/2] = sum_ci W[ci][co][s] x[ci][m] + W[ci][co][s+U] x[ci][m-1]
+  // -> conv weight w'[co*U + s][ci][tap]: tap 0 reads x[m-1], tap 1 reads x[m]
+  const int K = 2 * U;
+  std::vector<float> wc((size_t)U * Cout * Cin * 2);
+  for (int co = 0; co < Cout; ++co)
+    for (int s = 0; s < U; ++s)
+      for (int ci = 0; ci < Cin; ++ci) {
+        const float* src = w + ((int64_t)ci * Cout + co) * K;
+        float* dst = wc.data() + (((size_t)co * U + s) * Cin + ci) * 2;
+        dst[0] = src[s + U];
+        dst[1] = src[s];
+      }
+  return pack_conv1d_split(mode, wc.data(), U * Cout, Cin, 2, t, out);
 }
 
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t) {

@@ -136,7 +136,7 @@ SIGNATURES = {
     "tts_op_conv1d_num_tiles": (c_int, [c_int]),
     "tts_op_conv_transpose1d": (
         c_int,
-        [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p],
+        [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_void_p, c_void_p],
     ),
     "tts_op_conv_post": (
         c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p]
