@@ -274,12 +274,25 @@ def main():
     achieved = per_launch_flops / (avg_ms / 1e3) / 1e12
     total_flops = sum(r["flops"] for r in rows)
     traffic = None
+    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r01.json)
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             traffic = tj.get("per_launch_bytes", {}).get(f"{a.math_mode}:{fam_name}")
+            fwd_bytes = tj.get("per_launch_bytes", {}).get(f"{a.math_mode}:__forward__")
         except Exception:
             traffic = None
+    algo_bytes = sum(r["bytes"] for r in rows)  # compulsory activation/weight bytes per launch, summed
+    step_s = ms_per_step / 1e3
+    hbm = {
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "algorithmic_bytes_per_step": algo_bytes,
+        "algorithmic_frac": algo_bytes / step_s / 1e9 / HBM_PEAK_GBS,
+        "pmc_bytes_per_step": fwd_bytes,
+        "achieved": fwd_bytes / step_s / 1e9 if fwd_bytes else None,
+        "frac": fwd_bytes / step_s / 1e9 / HBM_PEAK_GBS if fwd_bytes else None,
+    }
 
     alt = None
     gens = {a.math_mode: g}
@@ -341,6 +354,7 @@ def main():
                 "flops_per_launch": per_launch_flops,
                 "avg_launch_ms": avg_ms,
             },
+            "hbm_roofline_step": hbm,
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
             "cpu_baseline": cpu,
             "alt_math_mode": alt,
