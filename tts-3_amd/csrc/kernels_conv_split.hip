@@ -338,6 +338,12 @@ constexpr ConvTile kSplitTiles[] = {
     {32, 256, 1, 2, 32, 2},   // 11
     {64, 128, 2, 1, 32, 3},   // 12
     {128, 128, 2, 2, 32, 2},  // 13
+    {32, 256, 1, 2, 16, 1},   // 14 small-LDS tiles for C <= 64 (2-3 workgroups per CU)
+    {32, 256, 1, 2, 16, 2},   // 15
+    {32, 128, 1, 1, 16, 2},   // 16
+    {64, 128, 2, 1, 16, 1},   // 17
+    {64, 128, 2, 1, 16, 2},   // 18
+    {32, 512, 1, 4, 16, 2},   // 19
 };
 constexpr int kNumSplitTiles = sizeof(kSplitTiles) / sizeof(kSplitTiles[0]);
 
@@ -371,6 +377,12 @@ void launch_split_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
     case 11: launch_split_t<S, K, 32, 256, 1, 2, 2, 2, false>(a, B, s); break;
     case 12: launch_split_t<S, K, 64, 128, 2, 1, 2, 3, false>(a, B, s); break;
     case 13: launch_split_t<S, K, 128, 128, 2, 2, 2, 2, false>(a, B, s); break;
+    case 14: launch_split_t<S, K, 32, 256, 1, 2, 1, 1, false>(a, B, s); break;
+    case 15: launch_split_t<S, K, 32, 256, 1, 2, 1, 2, false>(a, B, s); break;
+    case 16: launch_split_t<S, K, 32, 128, 1, 1, 1, 2, false>(a, B, s); break;
+    case 17: launch_split_t<S, K, 64, 128, 2, 1, 1, 1, false>(a, B, s); break;
+    case 18: launch_split_t<S, K, 64, 128, 2, 1, 1, 2, false>(a, B, s); break;
+    case 19: launch_split_t<S, K, 32, 512, 1, 4, 1, 2, false>(a, B, s); break;
     default: throw Error(3, "conv1d(split): bad tile index " + std::to_string(tile));
   }
 }
@@ -408,7 +420,7 @@ int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res)
   if (mode == MATH_FP32_F16X3) {
     if (Cout > 64) return 13;
     if (Cout > 32) return 10;
-    return 2;
+    return 14;  // one 16-channel group, 42 KB of LDS: 3 workgroups per CU
   }
   if (Cout > 64) return (K >= 11 || Cin % 32 != 0) ? 7 : 3;
   if (Cout > 32) return K <= 3 ? 10 : 1;
