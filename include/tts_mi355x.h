@@ -184,6 +184,43 @@ int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const floa
                                       TtsLaunchRecord* records, int max_records, int* n_records);
 
 /* ------------------------------------------------------------------------------------ */
+/* VITS flow: ResidualCouplingBlocks, reverse (TTS/tts/layers/vits/networks.py:169-232)     */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors ResidualCouplingBlocks.__init__ (networks.py:169-202; VITS builds it at
+ * vits.py:675-682 with mean-only blocks). */
+typedef struct TtsVitsFlowCfg {
+  int channels;        /* 192 (hidden_channels) */
+  int hidden_channels; /* 192 */
+  int kernel_size;     /* 5 (kernel_size_flow) */
+  int dilation_rate;   /* 1 (dilation_rate_flow) */
+  int num_layers;      /* 4 (num_layers_flow) */
+  int num_flows;       /* 4 */
+  int cond_channels;   /* speaker embedding size, 0 = none (embedded_speaker_dim) */
+  int math_mode;       /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
+} TtsVitsFlowCfg;
+
+/* Host weight order, per flow f < num_flows (weight norm folded: w = g * v / ||v||):
+ *   pre.weight [H][C/2], pre.bias [H]
+ *   for l < L: enc.in_layers.l.weight [2H][H][k], enc.in_layers.l.bias [2H]
+ *   for l < L: enc.res_skip_layers.l.weight [l<L-1 ? 2H : H][H], bias
+ *   if cond_channels: enc.cond_layer.weight [2*H*L][cond_channels], enc.cond_layer.bias [2*H*L]
+ *   post.weight [C/2][H], post.bias [C/2] */
+int tts_vits_flow_num_weights(const TtsVitsFlowCfg* cfg);
+int64_t tts_vits_flow_weight_numel(const TtsVitsFlowCfg* cfg, int index);
+int tts_vits_flow_create(const TtsVitsFlowCfg* cfg, const float* const* host_weights, int device,
+                         void** handle);
+int tts_vits_flow_destroy(void* handle);
+/* y[B][C][T] = ResidualCouplingBlocks(x, mask, g, reverse=True).  x, y: [B][C][T] fp32 (y may
+ * equal x: in place), mask: [B][T], g: [B][cond_channels] (NULL when cond_channels == 0).
+ * reverse must be 1. */
+int tts_vits_flow_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
+                          int C, int T, int reverse, float* d_y, void* hip_stream);
+int tts_vits_flow_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                                   int B, int C, int T, int reverse, float* d_y, void* hip_stream,
+                                   TtsLaunchRecord* records, int max_records, int* n_records);
+
+/* ------------------------------------------------------------------------------------ */
 /* Single-op entry points (test / tuning surface).  These pack the host weights into a     */
 /* temporary device buffer on every call and synchronise; they are not the hot path.        */
 /* ------------------------------------------------------------------------------------ */

@@ -1,7 +1,8 @@
 """Generate the golden fixtures under tests/golden/ by running the REFERENCE modules.
 
 Run in the development container only (it imports /root/reference, which does not exist on
-the GPU box):   python tests/golden/make_goldens.py
+the GPU box):   python tests/golden/make_goldens.py        (HiFiGAN + Glow fixtures)
+                python tests/golden/make_goldens.py vits   (VITS flow fixtures)
 
 Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
 but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
@@ -48,6 +49,13 @@ def import_reference():
     from TTS.tts.layers.glow_tts.decoder import Decoder
 
     return HifiganGenerator, Decoder
+
+
+def import_reference_vits_flow():
+    import_reference()
+    from TTS.tts.layers.vits.networks import ResidualCouplingBlocks
+
+    return ResidualCouplingBlocks
 
 
 def hifigan_case(HifiganGenerator, name, cfg, seed, B, T, mel_seed, stage_B=None, stage_T=None, with_forward=True):
@@ -136,7 +144,38 @@ def glow_case(Decoder, name, cfg, seed, B, T, lengths, x_seed):
           f"max|fp32-fp64| {np.abs(y32.numpy() - y64.numpy()).max():.2e}")
 
 
+def vits_flow_case(ResidualCouplingBlocks, name, cfg, seed, B, T, lengths, x_seed):
+    torch.manual_seed(0)
+    ref = ResidualCouplingBlocks(cfg["channels"], cfg["hidden_channels"], kernel_size=cfg["kernel_size"],
+                                 dilation_rate=cfg["dilation_rate"], num_layers=cfg["num_layers"],
+                                 num_flows=cfg["num_flows"], cond_channels=cfg["cond_channels"])
+    sd = synthetic.vits_flow_state_dict(**cfg, seed=seed)
+    ref.load_state_dict(sd)
+    ref.eval()
+    gen = torch.Generator().manual_seed(x_seed)
+    x = torch.randn(B, cfg["channels"], T, generator=gen)
+    g = torch.randn(B, cfg["cond_channels"], 1, generator=gen) if cfg["cond_channels"] else None
+    lengths_t = torch.tensor(lengths)
+    mask = (torch.arange(T)[None, :] < lengths_t[:, None]).float().unsqueeze(1)
+    with torch.no_grad():
+        y32 = ref(x, mask, g=g, reverse=True)
+        ref64 = ref.double()
+        y64 = ref64(x.double(), mask.double(), g=g.double() if g is not None else None, reverse=True)
+        z64 = ref64(y64, mask.double(), g=g.double() if g is not None else None, reverse=False)
+    meta = dict(kind="vits_flow", config=cfg, seed=seed, x_seed=x_seed, B=B, T=T, lengths=lengths)
+    arrays = dict(x=x.numpy(), mask=mask.numpy(), out_ref_fp32=y32.numpy(), out_ref_fp64=y64.numpy(),
+                  roundtrip_fp64=z64.numpy())
+    if g is not None:
+        arrays["g"] = g.numpy()
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: out {tuple(y32.shape)} std {y32.std():.4f} "
+          f"max|fp32-fp64| {np.abs(y32.numpy() - y64.numpy()).max():.2e}")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "vits":
+        return main_vits()
     HifiganGenerator, Decoder = import_reference()
     v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
@@ -166,6 +205,16 @@ def main():
                 num_coupling_layers=4, num_splits=4, num_squeeze=2)
     glow_case(Decoder, "glow_decoder_b2_t64", glow, seed=4321, B=2, T=64, lengths=[64, 41], x_seed=21)
     glow_case(Decoder, "glow_decoder_b3_t33", glow, seed=4322, B=3, T=33, lengths=[33, 20, 1], x_seed=22)
+
+
+def main_vits():
+    ResidualCouplingBlocks = import_reference_vits_flow()
+    # G5: VITS reverse flow (vits.py:675-682 defaults), ragged mask; and with a speaker embedding
+    flow = dict(channels=192, hidden_channels=192, kernel_size=5, dilation_rate=1, num_layers=4, num_flows=4,
+                cond_channels=0)
+    vits_flow_case(ResidualCouplingBlocks, "vits_flow_b2_t40", flow, seed=2468, B=2, T=40, lengths=[40, 27], x_seed=31)
+    vits_flow_case(ResidualCouplingBlocks, "vits_flow_cond_b3_t17", dict(flow, cond_channels=8), seed=2469, B=3,
+                   T=17, lengths=[17, 9, 1], x_seed=32)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from _util import goldens, max_abs, rel_rms
-from oracle import glow_ref, hifigan_ref
+from oracle import glow_ref, hifigan_ref, vits_ref
 from tts_amd import synthetic
 
 HIFI = goldens("hifigan")
@@ -80,6 +80,31 @@ def test_glow_reference_roundtrip_fixture(name, meta, arr):
     m = arr["mask"][:, :, 1:T2:2].repeat(2, axis=2)
     x = arr["x"][:, :, :T2] * m
     assert max_abs(arr["roundtrip_fp64"] * m, x) < 1e-4
+
+
+VITS = goldens("vits_flow")
+
+
+@pytest.mark.parametrize("name,meta,arr", VITS, ids=[g[0] for g in VITS])
+def test_vits_flow_oracle_matches_reference(name, meta, arr):
+    cfg = meta["config"]
+    sd = synthetic.vits_flow_state_dict(**cfg, seed=meta["seed"])
+    g = torch.from_numpy(arr["g"]) if "g" in arr else None
+    x, m = torch.from_numpy(arr["x"]), torch.from_numpy(arr["mask"])
+    out = vits_ref.vits_flow_reverse(sd, x, m, g, dtype=torch.float64, **cfg)
+    assert out.shape == arr["out_ref_fp64"].shape
+    assert max_abs(out.numpy(), arr["out_ref_fp64"]) < 1e-10
+    out32 = vits_ref.vits_flow_reverse(sd, x, m, g, dtype=torch.float32, **cfg)
+    assert max_abs(out32.numpy(), arr["out_ref_fp32"]) < 1e-5
+
+
+@pytest.mark.parametrize("name,meta,arr", VITS, ids=[g[0] for g in VITS])
+def test_vits_flow_reference_roundtrip_fixture(name, meta, arr):
+    # the reference's forward direction inverts its reverse on the unmasked frames; masked
+    # frames of x1 are zeroed by every block, so compare under the mask
+    m = arr["mask"]
+    assert max_abs(arr["roundtrip_fp64"] * m, arr["x"] * m) < 1e-9
+    assert len(VITS) == 2
 
 
 def test_synthetic_weights_deterministic():

@@ -1,0 +1,92 @@
+"""VITS reverse flow (ResidualCouplingBlocks, networks.py:169-232) on MI355X through the C-ABI,
+against the reference's own fp64 output (golden fixtures) and the CPU oracle; plus the VITS
+waveform path of config 5: flow -> z * mask -> HiFiGAN decoder (in 192, cond, no conv_post
+bias, no padding; vits.py:1156-1162)."""
+import numpy as np
+import pytest
+import torch
+
+from _util import assert_close_fp32, goldens
+from oracle import hifigan_ref, vits_ref
+from tts_amd import synthetic
+from tts_amd.config import VITS_DECODER, VITS_FLOW
+from tts_amd.tts import ResidualCouplingBlocks
+from tts_amd.vocoder import HifiganGenerator
+
+pytestmark = pytest.mark.gpu
+
+VITS = goldens("vits_flow")
+MODES = ["fp32", "fp32x6"]
+
+
+def build(cfg, seed, device, math_mode="fp32"):
+    f = ResidualCouplingBlocks(cfg["channels"], cfg["hidden_channels"], cfg["kernel_size"], cfg["dilation_rate"],
+                               cfg["num_layers"], num_flows=cfg["num_flows"], cond_channels=cfg["cond_channels"],
+                               math_mode=math_mode)
+    sd = synthetic.vits_flow_state_dict(**cfg, seed=seed)
+    f.load_state_dict(sd)
+    return f.to(device), sd
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name,meta,arr", VITS, ids=[g[0] for g in VITS])
+def test_vits_flow_vs_reference(cuda_device, name, meta, arr, mode):
+    f, _ = build(meta["config"], meta["seed"], cuda_device, mode)
+    g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
+    y = f(torch.from_numpy(arr["x"]).to(cuda_device), torch.from_numpy(arr["mask"]).to(cuda_device), g=g, reverse=True)
+    assert_close_fp32(y.cpu(), arr["out_ref_fp64"], f"{name} ({mode})")
+
+
+@pytest.mark.parametrize("cond", [0, 4])
+def test_vits_flow_vs_oracle_other_shapes(cuda_device, cond):
+    cfg = dict(VITS_FLOW, channels=64, hidden_channels=96, num_layers=3, num_flows=3, dilation_rate=2,
+               cond_channels=cond)
+    f, sd = build(cfg, 11 + cond, cuda_device)
+    gen = torch.Generator().manual_seed(5)
+    B, T = 3, 77
+    x = torch.randn(B, 64, T, generator=gen)
+    mask = (torch.arange(T)[None, :] < torch.tensor([77, 40, 3])[:, None]).float().unsqueeze(1)
+    g = torch.randn(B, cond, 1, generator=gen) if cond else None
+    ref = vits_ref.vits_flow_reverse(sd, x, mask, g, dtype=torch.float64, **cfg)
+    y = f(x.to(cuda_device), mask.to(cuda_device), g=g.to(cuda_device) if g is not None else None, reverse=True)
+    assert_close_fp32(y.cpu(), ref, f"vits flow cond={cond}")
+
+
+def test_vits_flow_batch_invariance_and_profile(cuda_device):
+    name, meta, arr = VITS[0]
+    f, _ = build(meta["config"], meta["seed"], cuda_device)
+    x = torch.from_numpy(arr["x"]).to(cuda_device)
+    m = torch.from_numpy(arr["mask"]).to(cuda_device)
+    y = f(x, m, reverse=True)
+    for i in range(x.shape[0]):
+        assert torch.equal(f(x[i : i + 1], m[i : i + 1], reverse=True)[0], y[i])
+    y2, rows = f.profile(x, m)
+    assert torch.equal(y2, y)
+    assert len(rows) == 4 * (2 + 4 * 4)  # pre, post, 4 x (in, gate, res_skip, update) per flow
+    assert all(r["ms"] > 0 for r in rows)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3"])
+def test_vits_waveform_path(cuda_device, mode):
+    """z = flow(z_p, mask, g, reverse); wav = decoder((z * mask), g)  (vits.py:1156-1162)."""
+    cond = 8
+    fcfg = dict(VITS_FLOW, cond_channels=cond)
+    flow, fsd = build(fcfg, 2469, cuda_device, "fp32" if mode == "f16x3" else mode)
+    dcfg = dict(VITS_DECODER, upsample_initial_channel=128, cond_channels=cond)
+    dsd = synthetic.hifigan_state_dict(**dcfg, seed=99, weight_norm=False)
+    dec = HifiganGenerator(**dcfg, math_mode=mode)
+    dec.remove_weight_norm()
+    dec.load_state_dict(dsd)
+    dec = dec.to(cuda_device)
+    gen = torch.Generator().manual_seed(9)
+    B, T = 2, 24
+    zp = torch.randn(B, 192, T, generator=gen)
+    mask = (torch.arange(T)[None, :] < torch.tensor([24, 13])[:, None]).float().unsqueeze(1)
+    g = torch.randn(B, cond, 1, generator=gen)
+    z = flow(zp.to(cuda_device), mask.to(cuda_device), g=g.to(cuda_device), reverse=True)
+    wav = dec(z * mask.to(cuda_device), g=g.to(cuda_device))
+    zr = vits_ref.vits_flow_reverse(fsd, zp, mask, g, dtype=torch.float64, **fcfg)
+    wr = hifigan_ref.hifigan_forward(dsd, zr * mask.double(), g=g.double(), pad=0, dtype=torch.float64, **dcfg)
+    assert_close_fp32(z.cpu(), zr, f"vits z ({mode})")
+    assert_close_fp32(wav.cpu(), wr, f"vits wav ({mode})")
+    assert np.isfinite(wav.cpu().numpy()).all()

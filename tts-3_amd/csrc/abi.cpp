@@ -9,6 +9,7 @@
 
 #include "glow.hpp"
 #include "hifigan.hpp"
+#include "vits.hpp"
 #include "tts_mi355x.h"
 
 namespace {
@@ -66,7 +67,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 103; }
+int tts_abi_version(void) { return 104; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -207,6 +208,68 @@ int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const floa
     {
       tts::DeviceGuard g(h->device());
       h->reverse(d_x, d_mask, B, C, T, d_y, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+// ----------------------------------------------------------------------------- VITS flow
+int tts_vits_flow_num_weights(const TtsVitsFlowCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_flow_validate(*cfg);
+    n = (int)tts::vits_flow_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_vits_flow_weight_numel(const TtsVitsFlowCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_flow_validate(*cfg);
+    auto s = tts::vits_flow_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_vits_flow_create(const TtsVitsFlowCfg* cfg, const float* const* host_weights, int device, void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::VitsFlow(*cfg, host_weights, device);
+  });
+}
+
+int tts_vits_flow_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::VitsFlow*>(handle); });
+}
+
+int tts_vits_flow_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B, int C,
+                          int T, int reverse, float* d_y, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    static_cast<tts::VitsFlow*>(handle)->reverse(d_x, d_mask, d_g, B, C, T, d_y, static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_flow_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
+                                   int C, int T, int reverse, float* d_y, void* hip_stream,
+                                   TtsLaunchRecord* records, int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    auto* h = static_cast<tts::VitsFlow*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);

@@ -63,6 +63,9 @@ struct Conv1dArgs {
   // (Tout = Tin + 1, pad = 1: taps x[m-1], x[m]); row rho, column m is stored at time
   // U*m + s - U/2 of y[b][co][0 .. U*Tin).  zmode 0, no res / mask / cvec.
   int ups;
+  int64_t o_bstride;     // floats between batch items of res / y / z (0 = Cout*Tout)
+  int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
+  int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
 };
 
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).

@@ -62,14 +62,16 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   const int Cout = a.Cout;
   const int Tout = a.Tout;
   const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;  // bytes of one batch item
-  const size_t item = (size_t)b * Cout * Tout;
+  const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
   const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
   const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
   const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
-  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * Cout : a.bias, a.cvec ? (unsigned)Cout * 4u : 0u);
+  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
+                               a.cvec ? (unsigned)Cout * 4u : 0u);
   const rsrc_t rmask = make_rsrc(a.mask ? a.mask + (size_t)b * Tout : a.bias, a.mask ? (unsigned)Tout * 4u : 0u);
   const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
   const bool has_mask = a.mask != nullptr;
+  const bool mask_res = RES && a.mask_res && has_mask;
   const float oslope = a.out_slope;
   const float zdiv = a.zdiv;
   const unsigned rowb = (unsigned)Tout * 4u;
@@ -92,6 +94,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
       // rows >= Cout land past the plane through the row term; columns >= Tout are marked OOB
       const unsigned voff = (t < Tout) ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
       const float mv = has_mask ? bload(rmask, (t < Tout ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
+      const float mv2 = mask_res ? mv : 1.f;  // (res + v) * mask for the VITS coupling update
       unsigned vo[16];
       float rv[16], zv[16];
 #pragma unroll
@@ -105,7 +108,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
       for (int r = 0; r < 16; ++r) {
         float v = (acc[m][n][r] + bv[r]) * mv;  // mv = 1 without a mask (exact)
         v = lrelu2(v, oslope);
-        if (RES) v += rv[r];
+        if (RES) v = (v + rv[r]) * mv2;  // mv2 = 1 unless mask_res (exact)
         if (ZM == 2) v = zv[r] + v;
         if (ZM == 3) v = (zv[r] + v) / zdiv;
         if (AMAX) vm = fmaxf(vm, fabsf(v));  // rows >= Cout hold exact zeros

@@ -33,6 +33,7 @@ void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipSt
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,
                            int Th, int first, int last, hipStream_t s);
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s);
+void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStream_t s);  // torch.flip(x, [1])
 
 class GlowDecoder {
  public:

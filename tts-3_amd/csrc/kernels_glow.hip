@@ -145,6 +145,22 @@ void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, i
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+// y[b][c][t] = x[b][C-1-c][t]  (torch.flip(x, [1]))
+__global__ __launch_bounds__(256) void channel_flip_kernel(const float* x, float* y, int C, int T) {
+  const int b = blockIdx.y;
+  const int64_t n = (int64_t)C * T;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i / T);
+    const int t = (int)(i - (int64_t)c * T);
+    y[(size_t)b * n + i] = x[(size_t)b * n + (int64_t)(C - 1 - c) * T + t];
+  }
+}
+
+void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStream_t s) {
+  hipLaunchKernelGGL(channel_flip_kernel, ew_grid((int64_t)C * T, B), dim3(256), 0, s, x, y, C, T);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
 void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s) {
   hipLaunchKernelGGL(glow_gate_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, xin, acts, H, Th);
   TTS_HIP_CHECK(hipGetLastError());

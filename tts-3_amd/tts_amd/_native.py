@@ -69,6 +69,19 @@ class TtsGlowDecoderCfg(Structure):
     ]
 
 
+class TtsVitsFlowCfg(Structure):
+    _fields_ = [
+        ("channels", c_int),
+        ("hidden_channels", c_int),
+        ("kernel_size", c_int),
+        ("dilation_rate", c_int),
+        ("num_layers", c_int),
+        ("num_flows", c_int),
+        ("cond_channels", c_int),
+        ("math_mode", c_int),
+    ]
+
+
 class TtsLaunchRecord(Structure):
     _fields_ = [("name", c_char * 48), ("flops", c_double), ("bytes", c_double), ("ms", c_float)]
 
@@ -123,6 +136,18 @@ SIGNATURES = {
     "tts_glow_decoder_forward_profiled": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_flow_num_weights": (c_int, [POINTER(TtsVitsFlowCfg)]),
+    "tts_vits_flow_weight_numel": (c_int64, [POINTER(TtsVitsFlowCfg), c_int]),
+    "tts_vits_flow_create": (c_int, [POINTER(TtsVitsFlowCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
+    "tts_vits_flow_destroy": (c_int, [c_void_p]),
+    "tts_vits_flow_forward": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]
+    ),
+    "tts_vits_flow_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_op_conv1d": (

@@ -3,6 +3,8 @@ JSON reader (no coqpit dependency).
 
 * ``HIFIGAN_V1``: ``HifiganConfig.generator_model_params`` (TTS/vocoder/configs/hifigan_config.py:95-104)
 * ``GLOW_TTS_DECODER``: the decoder fields of ``GlowTTSConfig`` (TTS/tts/configs/glow_tts_config.py:117-131)
+* ``VITS_FLOW`` / ``VITS_DECODER``: the flow and waveform-decoder fields of ``VitsArgs``
+  (TTS/tts/models/vits.py:545-565, built at :675-682 and :704-718)
 """
 from __future__ import annotations
 
@@ -30,6 +32,30 @@ GLOW_TTS_DECODER: Dict[str, Any] = {
     "num_squeeze": 2,
     "sigmoid_scale": False,
     "c_in_channels": 0,
+}
+
+VITS_FLOW: Dict[str, Any] = {
+    "channels": 192,            # hidden_channels
+    "hidden_channels": 192,
+    "kernel_size": 5,           # kernel_size_flow
+    "dilation_rate": 1,         # dilation_rate_flow
+    "num_layers": 4,            # num_layers_flow
+    "num_flows": 4,
+}
+
+VITS_DECODER: Dict[str, Any] = {
+    "in_channels": 192,
+    "out_channels": 1,
+    "resblock_type": "1",
+    "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+    "resblock_kernel_sizes": [3, 7, 11],
+    "upsample_kernel_sizes": [16, 16, 4, 4],
+    "upsample_initial_channel": 512,
+    "upsample_factors": [8, 8, 2, 2],
+    "inference_padding": 0,
+    "conv_pre_weight_norm": False,
+    "conv_post_weight_norm": False,
+    "conv_post_bias": False,
 }
 
 

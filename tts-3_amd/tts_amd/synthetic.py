@@ -23,7 +23,7 @@ from typing import Dict, List, Sequence
 import numpy as np
 import torch
 
-from .config import HIFIGAN_V1, GLOW_TTS_DECODER
+from .config import HIFIGAN_V1, GLOW_TTS_DECODER, VITS_FLOW
 
 
 def _wn_pair(rng, v: np.ndarray):
@@ -162,6 +162,54 @@ def glow_decoder_state_dict(
         for l in range(num_coupling_layers):
             rsc = 2 * H if l < num_coupling_layers - 1 else H
             wn_conv(f"flows.{cb}.wn.res_skip_layers.{l}", rsc, H, 1, 1.0)
+    return sd
+
+
+def vits_flow_state_dict(
+    channels: int = VITS_FLOW["channels"],
+    hidden_channels: int = VITS_FLOW["hidden_channels"],
+    kernel_size: int = VITS_FLOW["kernel_size"],
+    dilation_rate: int = VITS_FLOW["dilation_rate"],
+    num_layers: int = VITS_FLOW["num_layers"],
+    num_flows: int = VITS_FLOW["num_flows"],
+    cond_channels: int = 0,
+    seed: int = 2468,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a VITS ``ResidualCouplingBlocks`` flow (TTS/tts/layers/vits/networks.py:169-232,
+    mean-only blocks :103-166) with synthetic weights, in the reference's key order.
+
+    ``post`` (zero-initialised in the reference, :135-136) is randomised too, otherwise every
+    block is an identity map and parity says nothing.
+    """
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    half = channels // 2
+    H = hidden_channels
+
+    def conv(name: str, cout: int, cin: int, k: int, scale: float):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        sd[f"{name}.weight"] = torch.from_numpy(w.astype(np.float32))
+        sd[f"{name}.bias"] = torch.from_numpy((rng.standard_normal((cout,)) * 0.02).astype(np.float32))
+
+    def wn_conv(name: str, cout: int, cin: int, k: int, scale: float):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        sd[f"{name}.bias"] = torch.from_numpy((rng.standard_normal((cout,)) * 0.02).astype(np.float32))
+        g, v = _wn_pair(rng, w)
+        sd[f"{name}.parametrizations.weight.original0"] = torch.from_numpy(g)
+        sd[f"{name}.parametrizations.weight.original1"] = torch.from_numpy(v)
+
+    for f in range(num_flows):
+        pre = f"flows.{f}"
+        conv(f"{pre}.pre", H, half, 1, 1.0)
+        for l in range(num_layers):
+            wn_conv(f"{pre}.enc.in_layers.{l}", 2 * H, H, kernel_size, 1.0)
+        for l in range(num_layers):
+            rsc = 2 * H if l < num_layers - 1 else H
+            wn_conv(f"{pre}.enc.res_skip_layers.{l}", rsc, H, 1, 1.0)
+        if cond_channels > 0:
+            wn_conv(f"{pre}.enc.cond_layer", 2 * H * num_layers, cond_channels, 1, 0.5)
+        conv(f"{pre}.post", half, H, 1, 0.3)
     return sd
 
 

@@ -67,7 +67,8 @@ class InvConvNear(nn.Module):
 
 
 class WN(nn.Module):
-    """wavenet.py:16-123 (parameters only; conditioning not implemented)."""
+    """wavenet.py:16-123 (parameters only).  ``cond_layer`` (c_in_channels > 0) is registered after
+    ``dropout`` as in the reference, so state_dict keys and order match."""
 
     def __init__(self, in_channels, hidden_channels, kernel_size, dilation_rate, num_layers, c_in_channels=0,
                  dropout_p=0, weight_norm_=True):
@@ -85,7 +86,7 @@ class WN(nn.Module):
         self.res_skip_layers = nn.ModuleList()
         self.dropout = nn.Dropout(dropout_p)
         if c_in_channels > 0:
-            raise NotImplementedError("speaker-conditioned WN (c_in_channels > 0) is not implemented on MI355X")
+            self.cond_layer = weight_norm(nn.Conv1d(c_in_channels, 2 * hidden_channels * num_layers, 1), name="weight")
         for i in range(num_layers):
             dilation = dilation_rate**i
             padding = int((kernel_size * dilation - dilation) / 2)
@@ -96,7 +97,8 @@ class WN(nn.Module):
             self.res_skip_layers.append(weight_norm(nn.Conv1d(hidden_channels, rsc, 1), name="weight"))
 
     def remove_weight_norm(self):  # wavenet.py:117-123
-        for l in list(self.in_layers) + list(self.res_skip_layers):
+        extra = [self.cond_layer] if self.c_in_channels > 0 else []
+        for l in extra + list(self.in_layers) + list(self.res_skip_layers):
             if is_parametrized(l, "weight"):
                 remove_parametrizations(l, "weight")
 
