@@ -32,16 +32,19 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
 # ceiling of each math mode in algorithmic fp32 FLOP/s: fp32x6 issues 6 bf16 MFMA products
 # per fp32 multiply-accumulate, f16x3 3 fp16 products (same MFMA rate as bf16); see
 # include/tts_mi355x.h TTS_MATH_*
-MODE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS / 6.0, "f16x3": BF16_PEAK_TFLOPS / 3.0}
+MODE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS / 6.0, "f16x3": BF16_PEAK_TFLOPS / 3.0,
+             "bf16": BF16_PEAK_TFLOPS}
 PEAK_BASIS = {
     "fp32": "fp32 MFMA 157.3 TF",
     "fp32x6": "bf16 dense MFMA 2.5 PF / 6 products per fp32 MAC",
     "f16x3": "fp16 dense MFMA 2.5 PF / 3 products per fp32 MAC",
+    "bf16": "bf16 dense MFMA 2.5 PF",
 }
 DTYPE = {
     "fp32": "fp32",
     "fp32x6": "fp32 (bf16x6 split on bf16 MFMA, fp32 accumulate)",
     "f16x3": "fp32 (power-of-2 scaled fp16 hi/lo split on fp16 MFMA, fp32 accumulate)",
+    "bf16": "bf16 (bf16 MFMA operands, fp32 accumulate, fp32 activations)",
 }
 HBM_PEAK_GBS = 8000.0
 SAMPLE_RATE = 22050
@@ -313,7 +316,7 @@ def main():
     glow = None
     if rank == 0 and not a.no_glow:
         # the Glow decoder implements fp32 and fp32x6 (TTS_MATH_FP32_F16X3 is HiFiGAN-only)
-        glow_mode = "fp32x6" if a.math_mode == "f16x3" else a.math_mode
+        glow_mode = "fp32x6" if a.math_mode == "f16x3" else a.math_mode  # bf16 runs as is
         glow = glow_bench(dev, glow_mode, cpu=(world == 1 and not a.no_cpu_baseline))
 
     if rank == 0:

@@ -56,10 +56,14 @@ extern "C" {
  *                     ceiling).  The
  *                     scales come from max-abs statistics each producing kernel records; the
  *                     HiFiGAN executor runs conv_pre (user input, no statistics) in FP32_X6.
- *                     HiFiGAN only: the Glow decoder rejects it (TTS_ERR_UNSUPPORTED). */
+ *                     HiFiGAN only: the Glow decoder rejects it (TTS_ERR_UNSUPPORTED).
+ *   TTS_MATH_BF16     bf16 operands on v_mfma_f32_32x32x16_bf16 with fp32 accumulation and fp32
+ *                     activations in HBM (the bf16 arithmetic of configs 3 / 5; not fp32-faithful:
+ *                     ~2^-9 relative per product). */
 #define TTS_MATH_FP32 0
 #define TTS_MATH_FP32_X6 1
 #define TTS_MATH_FP32_F16X3 2
+#define TTS_MATH_BF16 3
 
 #define TTS_MAX_UPSAMPLES 8
 #define TTS_MAX_KERNELS 4
@@ -96,7 +100,7 @@ typedef struct TtsHifiganCfg {
   int inference_padding;                /* default 5 (:173) */
   int cond_channels;                    /* 0 = no cond_layer (:227-228) */
   int conv_post_bias;                   /* default 1 (:177) */
-  int math_mode;                        /* TTS_MATH_FP32 (default), _X6 or _F16X3 */
+  int math_mode;                        /* TTS_MATH_FP32 (default), _X6, _F16X3 or TTS_MATH_BF16 */
 } TtsHifiganCfg;
 
 /* Number of host weight tensors create() expects, and the element count of tensor idx.
@@ -158,7 +162,7 @@ typedef struct TtsGlowDecoderCfg {
   int num_squeeze;         /* 2 */
   int sigmoid_scale;       /* 0 */
   int c_in_channels;       /* 0 (speaker conditioning not implemented: must be 0) */
-  int math_mode;           /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
+  int math_mode;           /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
 } TtsGlowDecoderCfg;
 
 /* Host weight order, per flow block b < num_flow_blocks (flows 3b, 3b+1, 3b+2):
@@ -197,7 +201,7 @@ typedef struct TtsVitsFlowCfg {
   int num_layers;      /* 4 (num_layers_flow) */
   int num_flows;       /* 4 */
   int cond_channels;   /* speaker embedding size, 0 = none (embedded_speaker_dim) */
-  int math_mode;       /* TTS_MATH_FP32 (default) or TTS_MATH_FP32_X6 */
+  int math_mode;       /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
 } TtsVitsFlowCfg;
 
 /* Host weight order, per flow f < num_flows (weight norm folded: w = g * v / ||v||):

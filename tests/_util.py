@@ -14,6 +14,17 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 # reference itself: max 5.6e-7, rel-RMS 1e-6 on HiFiGAN; 2.9e-6 on the Glow decoder)
 FP32_MAX_ABS = 1e-4
 FP32_REL_RMS = 1e-5
+# bf16 math mode (TTS_MATH_BF16, configs 3 / 5): SURVEY.md §8c's bf16 gate; the reference's own
+# bf16 CPU forward measured rel-RMS 1.3e-2 and max 6.2e-3 vs fp64
+BF16_MAX_ABS = 1e-1
+BF16_REL_RMS = 3e-2
+
+
+def tol(mode: str) -> dict:
+    """Parity gates of a math mode (every mode but bf16 is held to the fp32 gates)."""
+    if mode == "bf16":
+        return dict(max_abs_tol=BF16_MAX_ABS, rel_rms_tol=BF16_REL_RMS)
+    return dict(max_abs_tol=FP32_MAX_ABS, rel_rms_tol=FP32_REL_RMS)
 
 
 def goldens(kind: str):

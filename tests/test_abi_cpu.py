@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 104
+    assert N.lib().tts_abi_version() == 105
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -170,7 +170,7 @@ def test_glow_config_validation():
 
 def test_math_modes_and_tile_tables():
     lib = N.lib()
-    assert N.MATH_MODES == {"fp32": 0, "fp32x6": 1, "f16x3": 2}
+    assert N.MATH_MODES == {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
     for m in N.MATH_MODES.values():
         assert lib.tts_op_conv1d_num_tiles(m) >= 3
     assert lib.tts_op_conv1d_num_tiles(7) == -N.TTS_ERR_INVALID

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from _util import assert_close_fp32, goldens, max_abs
+from _util import BF16_MAX_ABS, BF16_REL_RMS, assert_close_fp32, goldens, max_abs
 from oracle import glow_ref
 from tts_amd import synthetic
 from tts_amd.tts import Decoder
@@ -25,7 +25,7 @@ def build(cfg, seed, device, math_mode="fp32"):
     return d.to(device)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "bf16"])
 @pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
 def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
     d = build(meta["config"], meta["seed"], cuda_device, mode)
@@ -33,7 +33,10 @@ def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
     m = torch.from_numpy(arr["mask"]).to(cuda_device)
     y, logdet = d(x, m, reverse=True)
     assert logdet is None
-    assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, GLOW_MAX_ABS, GLOW_REL_RMS)
+    if mode == "bf16":
+        assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, BF16_MAX_ABS, BF16_REL_RMS)
+    else:
+        assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, GLOW_MAX_ABS, GLOW_REL_RMS)
 
 
 @pytest.mark.parametrize("B,T,lengths", [(1, 2, [2]), (2, 7, [7, 3]), (4, 400, [400, 399, 200, 1])])

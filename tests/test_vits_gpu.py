@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from _util import assert_close_fp32, goldens
+from _util import assert_close_fp32, goldens, tol
 from oracle import hifigan_ref, vits_ref
 from tts_amd import synthetic
 from tts_amd.config import VITS_DECODER, VITS_FLOW
@@ -16,7 +16,7 @@ from tts_amd.vocoder import HifiganGenerator
 pytestmark = pytest.mark.gpu
 
 VITS = goldens("vits_flow")
-MODES = ["fp32", "fp32x6"]
+MODES = ["fp32", "fp32x6", "bf16"]
 
 
 def build(cfg, seed, device, math_mode="fp32"):
@@ -34,7 +34,7 @@ def test_vits_flow_vs_reference(cuda_device, name, meta, arr, mode):
     f, _ = build(meta["config"], meta["seed"], cuda_device, mode)
     g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
     y = f(torch.from_numpy(arr["x"]).to(cuda_device), torch.from_numpy(arr["mask"]).to(cuda_device), g=g, reverse=True)
-    assert_close_fp32(y.cpu(), arr["out_ref_fp64"], f"{name} ({mode})")
+    assert_close_fp32(y.cpu(), arr["out_ref_fp64"], f"{name} ({mode})", **tol(mode))
 
 
 @pytest.mark.parametrize("cond", [0, 4])
@@ -66,7 +66,7 @@ def test_vits_flow_batch_invariance_and_profile(cuda_device):
     assert all(r["ms"] > 0 for r in rows)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3"])
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3", "bf16"])
 def test_vits_waveform_path(cuda_device, mode):
     """z = flow(z_p, mask, g, reverse); wav = decoder((z * mask), g)  (vits.py:1156-1162)."""
     cond = 8
@@ -87,6 +87,6 @@ def test_vits_waveform_path(cuda_device, mode):
     wav = dec(z * mask.to(cuda_device), g=g.to(cuda_device))
     zr = vits_ref.vits_flow_reverse(fsd, zp, mask, g, dtype=torch.float64, **fcfg)
     wr = hifigan_ref.hifigan_forward(dsd, zr * mask.double(), g=g.double(), pad=0, dtype=torch.float64, **dcfg)
-    assert_close_fp32(z.cpu(), zr, f"vits z ({mode})")
-    assert_close_fp32(wav.cpu(), wr, f"vits wav ({mode})")
+    assert_close_fp32(z.cpu(), zr, f"vits z ({mode})", **tol(mode))
+    assert_close_fp32(wav.cpu(), wr, f"vits wav ({mode})", **tol(mode))
     assert np.isfinite(wav.cpu().numpy()).all()

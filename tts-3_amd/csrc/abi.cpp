@@ -67,7 +67,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 104; }
+int tts_abi_version(void) { return 105; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -287,7 +287,7 @@ static void op_conv1d_impl(const TtsConv1dDesc* d, const float* d_x, const float
   TTS_REQUIRE(d->zmode >= 0 && d->zmode <= 3, 1, "bad zmode");
   TTS_REQUIRE(d->zmode == 0 ? d_y != nullptr : d_z != nullptr, 1, "missing output pointer");
   const int mode = d->math_mode;
-  TTS_REQUIRE(mode >= tts::MATH_FP32 && mode <= tts::MATH_FP32_F16X3, 1, "unknown math_mode");
+  TTS_REQUIRE(mode >= tts::MATH_FP32 && mode <= tts::MATH_LAST, 1, "unknown math_mode");
   if (tile < 0) tile = tts::conv_tile_for(mode, d->Cout, d->K, d->Cin, d->dil, d_res != nullptr);
   const tts::ConvTile t = tts::conv_tile(mode, tile);
   std::vector<float> packed(tts::packed_conv_numel(mode, d->Cout, d->Cin, d->K, t));
@@ -343,7 +343,7 @@ int tts_op_conv1d_bench(const TtsConv1dDesc* d, const float* d_x, const float* h
 }
 
 int tts_op_conv1d_num_tiles(int math_mode) {
-  if (math_mode < tts::MATH_FP32 || math_mode > tts::MATH_FP32_F16X3) {
+  if (math_mode < tts::MATH_FP32 || math_mode > tts::MATH_LAST) {
     g_last_error = "unknown math_mode";
     return -TTS_ERR_INVALID;
   }
@@ -358,7 +358,7 @@ int tts_op_conv_transpose1d(const float* d_x, int B, int Cin, int Tin, const flo
     TTS_REQUIRE(B >= 1 && Cin >= 1 && Cout >= 1 && Tin >= 1, 1, "bad conv_transpose1d shape");
     TTS_REQUIRE(K == 2 * stride, 3, "conv_transpose1d: requires kernel_size == 2*stride");
     TTS_REQUIRE(stride == 2 || stride == 4 || stride == 8, 3, "conv_transpose1d: stride must be 2, 4 or 8");
-    TTS_REQUIRE(math_mode >= tts::MATH_FP32 && math_mode <= tts::MATH_FP32_F16X3, 1, "unknown math_mode");
+    TTS_REQUIRE(math_mode >= tts::MATH_FP32 && math_mode <= tts::MATH_LAST, 1, "unknown math_mode");
     auto s = static_cast<hipStream_t>(hip_stream);
     if (tts::is_split_mode(math_mode)) {
       const int tile = tts::conv_tile_for(math_mode, stride * Cout, 2, Cin, 1, false);

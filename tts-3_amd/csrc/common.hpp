@@ -113,6 +113,8 @@ void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cv
 constexpr int MATH_FP32 = 0;        // v_mfma_f32_32x32x2_f32
 constexpr int MATH_FP32_X6 = 1;     // bf16x6 split on v_mfma_f32_32x32x16_bf16
 constexpr int MATH_FP32_F16X3 = 2;  // scaled fp16 hi/lo split on v_mfma_f32_32x32x16_f16
+constexpr int MATH_BF16 = 3;        // bf16 operands, fp32 accumulation, fp32 activations in HBM
+constexpr int MATH_LAST = MATH_BF16;
 
 // Split-precision conv1d (kernels_conv_split.hip), mode MATH_FP32_X6 or MATH_FP32_F16X3.
 ConvTile conv1d_split_tile(int mode, int idx);
@@ -123,7 +125,7 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile_i
 void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s);
 
 // Mode-dispatching helpers used by the executors and the op entry points.
-inline bool is_split_mode(int mode) { return mode == MATH_FP32_X6 || mode == MATH_FP32_F16X3; }
+inline bool is_split_mode(int mode) { return mode == MATH_FP32_X6 || mode == MATH_FP32_F16X3 || mode == MATH_BF16; }
 inline ConvTile conv_tile(int mode, int idx) {
   return is_split_mode(mode) ? conv1d_split_tile(mode, idx) : conv1d_tile(idx);
 }

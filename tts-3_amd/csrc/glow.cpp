@@ -50,9 +50,9 @@ void glow_validate(const TtsGlowDecoderCfg& c) {
     d *= c.dilation_rate;
   }
   TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned Glow decoder (c_in_channels > 0) not implemented");
-  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_FP32_F16X3, 1, "unknown math_mode");
+  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
   TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3,
-              "Glow decoder: math_mode FP32_F16X3 is not implemented (use FP32 or FP32_X6)");
+              "Glow decoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
 GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, int device)

@@ -77,7 +77,7 @@ void hifigan_validate(const TtsHifiganCfg& c) {
   }
   TTS_REQUIRE(c.inference_padding >= 0, 1, "inference_padding must be >= 0");
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
-  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_FP32_F16X3, 1, "unknown math_mode");
+  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
 }
 
 // ---------------------------------------------------------------------------------------

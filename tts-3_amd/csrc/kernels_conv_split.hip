@@ -80,6 +80,22 @@ struct SchemeH3 {
   }
 };
 
+// Plain bf16 (MATH_BF16): one bf16 piece per operand, one product, fp32 accumulation.
+struct SchemeB1 {
+  static constexpr int NP = 1;
+  static constexpr int ROWB = 48;     // 32 B + 16 B pad (conflict-free like the other pitches)
+  static constexpr int NACC = 1;
+  static constexpr int NPROD = 1;
+  static constexpr int PA[1] = {0};
+  static constexpr int PB[1] = {0};
+  static constexpr int PACC[1] = {0};
+  static constexpr bool SCALED = false;
+  __device__ static __forceinline__ void split(float x, unsigned short (&p)[1]) { p[0] = bf16_bits((__bf16)x); }
+  __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
 // Exponent e such that max|x| * 2^-e lies in [2^13, 2^14): read the 64 max-abs slots the
 // producer published (one per lane), wave max, frexp.  No statistics, zero or non-finite max:
 // e = 0 (an overflowing input then yields inf, as fp16 would; NaN propagates).
@@ -436,6 +452,7 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, 
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
   if (mode == MATH_FP32_F16X3) launch_split_s<SchemeH3>(a, B, K, tile, s);
+  else if (mode == MATH_BF16) launch_split_s<SchemeB1>(a, B, K, tile, s);
   else launch_split_s<SchemeX6>(a, B, K, tile, s);
   TTS_HIP_CHECK(hipGetLastError());
 }

@@ -65,7 +65,7 @@ static inline void split_h3_host(float x, uint16_t& hi, uint16_t& lo) {
   lo = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)h));
 }
 
-static int split_pieces(int mode) { return mode == MATH_FP32_F16X3 ? 2 : 3; }
+static int split_pieces(int mode) { return mode == MATH_FP32_F16X3 ? 2 : (mode == MATH_BF16 ? 1 : 3); }
 
 // Split-mode A-operand fragments (conv1d_split_kernel), in floats (2 x 16-bit per float):
 //   out[mb][c16][k][piece][lane][j] = piece_p(w'[mb*32 + (lane&31)][c16*16 + 8*(lane>>5) + j][k])
@@ -104,7 +104,8 @@ int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const 
             const int ci = c16 * 16 + 8 * (lane >> 5) + j;
             const float v = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
             if (NP == 3) split3_host(v, pc[0][lane][j], pc[1][lane][j], pc[2][lane][j]);
-            else split_h3_host(std::ldexp(v, -e), pc[0][lane][j], pc[1][lane][j]);
+            else if (NP == 2) split_h3_host(std::ldexp(v, -e), pc[0][lane][j], pc[1][lane][j]);
+            else pc[0][lane][j] = f2bf_rne(v);
           }
         for (int p = 0; p < NP; ++p)
           for (int lane = 0; lane < 64; ++lane)

@@ -60,8 +60,8 @@ void vits_flow_validate(const TtsVitsFlowCfg& c) {
     d *= c.dilation_rate;
   }
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
-  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_FP32_F16X3, 1, "unknown math_mode");
-  TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3, "VITS flow: math_mode FP32_F16X3 is not implemented (use FP32 or FP32_X6)");
+  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
+  TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3, "VITS flow: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
 VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device) : cfg_(cfg), device_(device) {

@@ -26,7 +26,7 @@ TTS_ERR_UNSUPPORTED = 3
 TTS_ERR_OOM = 4
 
 # math modes (TTS_MATH_* in tts_mi355x.h)
-MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2}
+MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
 MAX_UPSAMPLES = 8
 MAX_KERNELS = 4
