@@ -68,6 +68,17 @@ struct Conv1dArgs {
   int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
 };
 
+// One fused ResBlock1 iteration (kernels_resblock.hip): c1 = convs1[m] (x, weights, dilation,
+// lrelu slopes, f16x3 input statistics), c2 = convs2[m] (weights, res = the iteration's input x,
+// output y or the MRF z, statistics of the output).  x and c2's output must not alias.
+struct ResPairArgs {
+  Conv1dArgs c1;
+  Conv1dArgs c2;
+};
+bool resblock_pair_supported(int mode, int C, int K, int dil);
+bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster
+void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
+
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
 struct ConvTile {
   int BM, BN, TM, TN, CK;

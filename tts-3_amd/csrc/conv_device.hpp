@@ -56,7 +56,7 @@ __device__ __forceinline__ void publish_amax(unsigned* slots, int b, float v) {
 
 template <int TM, int TN, bool RES, int ZM, bool AMAX>
 __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
-                                                   int tbase, int cobase, int lane) {
+                                                   int tbase, int cobase, int lane, int tend) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int Cout = a.Cout;
@@ -91,9 +91,11 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
     for (int n = 0; n < TN; ++n) {
       const int t = tbase + n * 32 + l32;
       const int row0 = cobase + m * 32 + 4 * half;
-      // rows >= Cout land past the plane through the row term; columns >= Tout are marked OOB
-      const unsigned voff = (t < Tout) ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-      const float mv = has_mask ? bload(rmask, (t < Tout ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
+      // rows >= Cout land past the plane through the row term; columns >= min(Tout, tend) are
+      // marked OOB
+      const bool tok = t < Tout && t < tend;
+      const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+      const float mv = has_mask ? bload(rmask, (tok ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
       const float mv2 = mask_res ? mv : 1.f;  // (res + v) * mask for the VITS coupling update
       unsigned vo[16];
       float rv[16], zv[16];
@@ -114,7 +116,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
         if (AMAX) vm = fmaxf(vm, fabsf(v));  // rows >= Cout hold exact zeros
         bstore(rout, v, vo[r], 0u);
       }
-      if (AMAX && t < Tout) vmax = fmaxf(vmax, vm);
+      if (AMAX && tok) vmax = fmaxf(vmax, vm);
     }
   }
   if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
@@ -168,18 +170,18 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 // unrolled epilogue carries no per-element branches.
 template <int TM, int TN, bool AMAX = false>
 __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
-                                              int tbase, int cobase, int lane) {
+                                              int tbase, int cobase, int lane, int tend = 0x7fffffff) {
   // copy the argument block: a store through `out` could alias it in the compiler's view
   const Conv1dArgs a = args;
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
   if (a.res) {
-    if (zm == 0) conv_epilogue_impl<TM, TN, true, 0, AMAX>(a, acc, b, tbase, cobase, lane);
-    else if (zm == 2) conv_epilogue_impl<TM, TN, true, 2, AMAX>(a, acc, b, tbase, cobase, lane);
-    else conv_epilogue_impl<TM, TN, true, 3, AMAX>(a, acc, b, tbase, cobase, lane);
+    if (zm == 0) conv_epilogue_impl<TM, TN, true, 0, AMAX>(a, acc, b, tbase, cobase, lane, tend);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, true, 2, AMAX>(a, acc, b, tbase, cobase, lane, tend);
+    else conv_epilogue_impl<TM, TN, true, 3, AMAX>(a, acc, b, tbase, cobase, lane, tend);
   } else {
-    if (zm == 0) conv_epilogue_impl<TM, TN, false, 0, AMAX>(a, acc, b, tbase, cobase, lane);
-    else if (zm == 2) conv_epilogue_impl<TM, TN, false, 2, AMAX>(a, acc, b, tbase, cobase, lane);
-    else conv_epilogue_impl<TM, TN, false, 3, AMAX>(a, acc, b, tbase, cobase, lane);
+    if (zm == 0) conv_epilogue_impl<TM, TN, false, 0, AMAX>(a, acc, b, tbase, cobase, lane, tend);
+    else if (zm == 2) conv_epilogue_impl<TM, TN, false, 2, AMAX>(a, acc, b, tbase, cobase, lane, tend);
+    else conv_epilogue_impl<TM, TN, false, 3, AMAX>(a, acc, b, tbase, cobase, lane, tend);
   }
 }
 

@@ -4,6 +4,7 @@
 // on the caller's stream.
 #include "hifigan.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -92,6 +93,12 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   // 1) describe layers, 2) size the arena, 3) pack on host, 4) one upload.
   const int C0 = cfg_.upsample_initial_channel;
   const int mode = cfg_.math_mode;
+  // TTS_MI355X_NO_PAIR_FUSION=1 keeps every resblock conv a separate launch (A/B measurements);
+  // TTS_MI355X_PAIR_FUSION=all fuses every supported iteration (not only the measured-faster ones)
+  const char* nf = std::getenv("TTS_MI355X_NO_PAIR_FUSION");
+  const bool pair_fusion = !(nf && nf[0] == '1');
+  const char* fa = std::getenv("TTS_MI355X_PAIR_FUSION");
+  const bool fuse_all = fa && std::string(fa) == "all";
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
@@ -143,11 +150,20 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         const float* w1[3]; const float* b1[3]; const float* w2[3]; const float* b2[3];
         for (int m = 0; m < 3; ++m) { w1[m] = hw[wi]; b1[m] = hw[wi + 1]; wi += 2; }
         for (int m = 0; m < 3; ++m) { w2[m] = hw[wi]; b2[m] = hw[wi + 1]; wi += 2; }
+        // fused convs1 -> convs2 iterations (kernels_resblock.hip) where supported; they reuse the
+        // conv packing, which needs 32-row blocks covering the channels and 16-channel groups
+        rb.fused = pair_fusion;
         for (int m = 0; m < 3; ++m) {
           rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false, mode));
           src.push_back({w1[m], b1[m]});
           rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true, mode));
           src.push_back({w2[m], b2[m]});
+          for (int c = 0; c < 2; ++c) {
+            const ConvTile t = conv_tile(mode, rb.convs[2 * m + c].tile);
+            const int dil = rb.convs[2 * m].dil;
+            rb.fused = rb.fused && (fuse_all ? resblock_pair_supported(mode, ch, k, dil) : resblock_pair_preferred(mode, ch, k, dil)) && t.CK == 16 &&
+                       ceil_div(ch, t.BM) * t.BM == ch;
+          }
         }
       } else {
         for (int m = 0; m < 2; ++m) {
@@ -356,7 +372,34 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
       const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
       const int gz = g0 + 1 + cfg_.num_kernels * 6;  // the stage's z / num_kernels
-      if (cfg_.resblock_type == 1) {
+      if (cfg_.resblock_type == 1 && rb.fused) {
+        // x_{m+1} = convs2[m](lrelu(convs1[m](lrelu(x_m)))) + x_m in one launch per m; the
+        // iterates ping-pong between X and T (o -> X -> T -> X / the MRF z)
+        for (int m = 0; m < 3; ++m) {
+          const ConvLayer& L1 = rb.convs[2 * m];
+          const ConvLayer& L2 = rb.convs[2 * m + 1];
+          const float* xin = (m == 0) ? bufO : (m == 1 ? bufX : bufT);
+          float* xout = (m == 1) ? bufT : bufX;
+          const bool last = (m == 2);
+          ResPairArgs pa{};
+          Conv1dArgs& c1 = pa.c1;
+          c1.x = xin; c1.w = L1.w; c1.bias = L1.b; c1.Cin = L1.Cin; c1.Cout = L1.Cout; c1.Tin = len; c1.Tout = len;
+          c1.dil = L1.dil; c1.pad = L1.pad; c1.n_chunks = L1.n_chunks; c1.in_slope = 0.1f; c1.out_slope = 0.1f;
+          c1.zdiv = 1.f; c1.w_exp = L1.w_exp;
+          c1.amax_in = (m == 0) ? slots(g0) : slots(gj + 2 * m - 1);
+          Conv1dArgs& c2 = pa.c2;
+          c2.x = nullptr; c2.w = L2.w; c2.bias = L2.b; c2.res = xin; c2.y = xout; c2.z = bufZ;
+          c2.Cin = L2.Cin; c2.Cout = L2.Cout; c2.Tin = len; c2.Tout = len; c2.dil = 1; c2.pad = L2.pad;
+          c2.n_chunks = L2.n_chunks; c2.in_slope = 1.f; c2.out_slope = 1.f; c2.zmode = last ? zlast : 0;
+          c2.zdiv = (float)cfg_.num_kernels; c2.w_exp = L2.w_exp;
+          c2.amax_out = last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1);
+          const double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
+          const double bytes = 4.0 * ((double)B * L1.Cout * len * (last ? (zlast >= 2 ? 4 : 3) : 3) +
+                                      2.0 * L1.Cout * L1.Cin * L1.K);
+          const std::string nm = "mrf_pair_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
+          run(prof, s, nm.c_str(), flops, bytes, [&] { launch_resblock_pair(L1.mode, pa, B, L1.K, L1.Cout, s); });
+        }
+      } else if (cfg_.resblock_type == 1) {
         for (int m = 0; m < 3; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;
           const unsigned* xin_amax = (m == 0) ? slots(g0) : slots(gj + 2 * m - 1);

@@ -1,0 +1,350 @@
+// Fused ResBlock1 iteration (TTS/vocoder/models/hifigan_generator.py:93-98) for C in {32, 64}:
+//   xt = convs1[m](lrelu(x, 0.1)); xt = lrelu(xt, 0.1); x' = convs2[m](xt) + x   [MRF z, :255-261]
+// in one kernel, so the intermediate xt never reaches HBM (per iteration the unfused path moves
+// five C-channel planes, this one three: x read twice, x' written once).
+//
+// A workgroup (4 waves) owns RP_BN = 224 output columns.  Phase 1 computes convs1 on RP_W = 256
+// columns (the 224 plus conv2's halo of up to 16 on each side, 2 blocks of 32 per wave), exactly
+// like conv1d_split_kernel (X staged per 16-channel chunk in LDS, weights streamed from L2).
+// Its epilogue applies the bias and the lrelu, zeroes columns outside [0, T) (conv2's zero
+// padding), splits the values into the scheme's pieces and stores them as conv2's B operand in
+// the LDS the X staging used.  Phase 2 runs convs2 over the same 256 columns from that buffer
+// (the last 32 are discarded) and finishes in conv_epilogue (bias, residual, MRF sum, statistics).
+// f16x3: xt's scale is the workgroup's own power of two (block max-abs): every conv2 output sums
+// products of one workgroup's xt only, so the per-tile scale is exact and batch-invariant.
+// The residual x is re-read from global memory, so x and x' must not alias (ping-pong buffers).
+#include "split_device.hpp"
+
+namespace tts {
+
+constexpr int RP_W = 256;    // convs1 columns per workgroup
+constexpr int RP_BN = 224;   // output columns per workgroup
+constexpr int RP_LEAD = 16;  // xt row 0 holds time t0 - RP_LEAD
+
+template <class S, int K, int C, int PD>
+struct PairCfg {
+  static constexpr int TM = C / 32;
+  static constexpr int TN = 2;
+  static constexpr int NC = C / 16;               // 16-channel groups
+  static constexpr int HMAX = (K - 1) * 5;        // dilation <= 5
+  static constexpr int XROWS = RP_W + HMAX;
+  static constexpr int XSZB = XROWS * S::ROWB;    // one X staging buffer (16 channels)
+  static constexpr int TROWS = RP_W + 32;         // + zero rows read by the discarded columns
+  static constexpr int TSZB = NC * TROWS * S::ROWB;
+  static constexpr int LDSB = (2 * XSZB > TSZB ? 2 * XSZB : TSZB);
+  static constexpr int UPT = (XROWS * 4 + 255) / 256;
+  static_assert((K - 1) / 2 <= RP_LEAD && RP_W - RP_BN == 2 * RP_LEAD, "conv2 halo");
+};
+
+template <class S, int K, int C, int PD>
+__global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
+  using P = PairCfg<S, K, C, PD>;
+  constexpr int NP = S::NP;
+  constexpr bool H3 = S::SCALED;
+  constexpr int TM = P::TM, TN = P::TN, NC = P::NC;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
+  __shared__ float red[4];
+
+  const Conv1dArgs& a1 = pa.c1;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int t0 = blockIdx.x * RP_BN;
+  const int b = blockIdx.z;
+  const int d = a1.dil;
+  const int T = a1.Tout;
+  const int XW = RP_W + (K - 1) * d;
+  const int tx0 = t0 - RP_LEAD;  // time of convs1 column 0
+  const unsigned avoff = (unsigned)lane * 16u;
+
+  // ------------------------------------------------------------------ phase 1: convs1
+  const int ex = H3 ? amax_exp(a1.amax_in, b) : 0;
+  const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;
+  const float* xb = a1.x + (size_t)b * C * T;
+  const unsigned chb = (unsigned)T * 4u;
+  unsigned uvoff[P::UPT];
+  int ulds[P::UPT];
+#pragma unroll
+  for (int i = 0; i < P::UPT; ++i) {
+    const int u = tid + i * 256;
+    const int q = u & 3;
+    const int r = u >> 2;
+    const int ts = tx0 - a1.pad + r;
+    const bool ok = r < XW && ts >= 0 && ts < T;
+    uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+    ulds[i] = r < XW ? r * S::ROWB + 8 * q : -1;
+  }
+  f32x4 xreg[P::UPT];
+  auto load_x = [&](int c) {
+    const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * T, (unsigned)(C - c * 16) * chb);
+#pragma unroll
+    for (int i = 0; i < P::UPT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
+  };
+  auto store_x = [&](int buf) {
+    unsigned char* xl = smem + buf * P::XSZB;
+#pragma unroll
+    for (int i = 0; i < P::UPT; ++i) {
+      if (ulds[i] >= 0) {
+        u16x4 pv[NP];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned short h[NP];
+          float v = lrelu2(xreg[i][j], a1.in_slope);
+          if (H3) v *= xscale;
+          S::split(v, h);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(xl + ulds[i] + 32 * p) = pv[p];
+      }
+    }
+  };
+
+  rsrc_t ra[TM];
+#pragma unroll
+  for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a1.w + ((size_t)m * NC * K) * (NP * 256), 0xFFFFFFFFu);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
+
+  f32x4 ar[PD + 1][TM][NP], bcur[TN][NP], bnext[TN][NP];
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
+
+  auto mfma_step = [&]() {
+#pragma unroll
+    for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+          acc[m][n] = S::mfma(ar[0][m][S::PA[e]], bcur[n][S::PB[e]], acc[m][n]);
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
+  };
+
+  const int xrow0 = wave * 64 + l32;
+  auto read_x = [&](const unsigned char* xl, int k, f32x4 (*dst)[NP]) {
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const unsigned char* p = xl + (xrow0 + n * 32 + k * d) * S::ROWB + 16 * half;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
+    }
+  };
+
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const unsigned char* xl = smem + (c & 1) * P::XSZB;
+    if (c + 1 < NC) load_x(c + 1);
+    read_x(xl, 0, bcur);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int s = c * K + k;
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((s + PD) * NP + q) * 1024u);
+      if (k + 1 < K) read_x(xl, k + 1, bnext);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_step();
+      if (k + 1 < K) {
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+      }
+    }
+    if (c + 1 < NC) store_x((c + 1) & 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ convs1 epilogue -> xt (LDS)
+  {
+    const float sc1 = H3 ? ldexpf(1.f, ex + a1.w_exp) : 1.f;
+    const rsrc_t rb1 = make_rsrc(a1.bias, (unsigned)C * 4u);
+    float tmax = 0.f;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      float bv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bv[r] = bload(rb1, (unsigned)(m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int t = tx0 + xrow0 + n * 32;
+        const bool inside = t >= 0 && t < T;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = lrelu2(acc[m][n][r] * sc1 + bv[r], a1.out_slope);
+          v = inside ? v : 0.f;
+          acc[m][n][r] = v;
+          tmax = fmaxf(tmax, fabsf(v));
+        }
+      }
+    }
+    float tscale = 1.f;
+    int et = 0;
+    if (H3) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+      if (lane == 0) red[wave] = tmax;
+      __syncthreads();
+      const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (mx > 0.f && mx < INFINITY) {
+        int E;
+        (void)frexpf(mx, &E);
+        et = E - 14;
+      }
+      tscale = ldexpf(1.f, -et);
+    }
+    // xt pieces: row = convs1 column, group = co / 16; registers r, r+1 (r even) are channels
+    // co, co+1 -> one 32-bit store per piece
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int row = xrow0 + n * 32;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          unsigned short h0[NP], h1[NP];
+          S::split(acc[m][n][r] * tscale, h0);
+          S::split(acc[m][n][r + 1] * tscale, h1);
+          unsigned char* dst = smem + ((co >> 4) * P::TROWS + row) * S::ROWB + 2 * (co & 15);
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            *reinterpret_cast<unsigned*>(dst + 32 * p) = (unsigned)h0[p] | ((unsigned)h1[p] << 16);
+        }
+      }
+    // zero rows RP_W .. TROWS-1 of every group (read only by the discarded columns)
+    constexpr int ZB = (P::TROWS - RP_W) * S::ROWB;  // bytes per group
+    for (int e = tid * 16; e < NC * ZB; e += 256 * 16) {
+      const int g = e / ZB;
+      *reinterpret_cast<f32x4*>(smem + (g * P::TROWS + RP_W) * S::ROWB + (e - g * ZB)) = f32x4{};
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase 2: convs2 from LDS
+    const Conv1dArgs& a2 = pa.c2;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a2.w + ((size_t)m * NC * K) * (NP * 256), 0xFFFFFFFFu);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
+    const int trow0 = xrow0 + RP_LEAD - (K - 1) / 2;
+    auto read_t = [&](int g, int k, f32x4 (*dst)[NP]) {
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const unsigned char* p = smem + (g * P::TROWS + trow0 + n * 32 + k) * S::ROWB + 16 * half;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
+      }
+    };
+    read_t(0, 0, bcur);
+#pragma unroll
+    for (int g = 0; g < NC; ++g) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int s = g * K + k;
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((s + PD) * NP + q) * 1024u);
+        const bool more = (k + 1 < K) || (g + 1 < NC);
+        if (more) read_t((k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_step();
+        if (more) {
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+        }
+      }
+    }
+    if (H3) {
+      const float sc2 = ldexpf(1.f, et + a2.w_exp);
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n) acc[m][n] *= sc2;
+    }
+    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wave * 64, 0, lane, t0 + RP_BN);
+  }
+}
+
+namespace {
+template <class S, int K, int C>
+void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
+  dim3 grid(ceil_div(a.c1.Tout, RP_BN), 1, B);
+  hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2>), grid, dim3(256), 0, s, a);
+}
+
+template <class S, int K>
+void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
+  if (C == 32) launch_pair_t<S, K, 32>(a, B, s);
+  else if (C == 64) launch_pair_t<S, K, 64>(a, B, s);
+  else throw Error(3, "resblock pair: channels must be 32 or 64");
+}
+
+template <class S>
+void launch_pair_s(const ResPairArgs& a, int B, int K, int C, hipStream_t s) {
+  switch (K) {
+    case 3: launch_pair_k<S, 3>(a, B, C, s); break;
+    case 7: launch_pair_k<S, 7>(a, B, C, s); break;
+    case 11: launch_pair_k<S, 11>(a, B, C, s); break;
+    default: throw Error(3, "resblock pair: kernel size must be 3, 7 or 11");
+  }
+}
+}  // namespace
+
+bool resblock_pair_supported(int mode, int C, int K, int dil) {
+  return is_split_mode(mode) && (C == 32 || C == 64) && (K == 3 || K == 7 || K == 11) && dil >= 1 && dil <= 5;
+}
+
+// Where the fused form is the faster one (MI355X A/B, scripts/ab_fusion.sh, f16x3): every
+// 32-channel iteration (-21..-37%); at 64 channels only k3 (-6%): the k7/k11 iterations are
+// MFMA-heavier and the 141 KB of LDS (xt for 64 channels) leaves one workgroup per CU.
+bool resblock_pair_preferred(int mode, int C, int K, int dil) {
+  return resblock_pair_supported(mode, C, K, dil) && (C == 32 || K == 3);
+}
+
+void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s) {
+  TTS_REQUIRE(resblock_pair_supported(mode, C, K, a.c1.dil), 3, "resblock pair: unsupported configuration");
+  TTS_REQUIRE(a.c1.Cin == C && a.c1.Cout == C && a.c2.Cin == C && a.c2.Cout == C && a.c1.Tin == a.c1.Tout &&
+                  a.c2.Tout == a.c1.Tout && a.c1.rep_pad == 0 && a.c2.dil == 1,
+              1, "resblock pair: bad arguments");
+  TTS_REQUIRE(a.c2.res != a.c2.y || a.c2.zmode != 0, 1, "resblock pair: x and x' must not alias");
+  TTS_REQUIRE((int64_t)C * a.c1.Tout * 4 < (int64_t(1) << 31), 3, "resblock pair: plane exceeds 2 GiB");
+  if (mode == MATH_FP32_F16X3) launch_pair_s<SchemeH3>(a, B, K, C, s);
+  else if (mode == MATH_BF16) launch_pair_s<SchemeB1>(a, B, K, C, s);
+  else launch_pair_s<SchemeX6>(a, B, K, C, s);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tts

@@ -1,0 +1,94 @@
+// Split-precision operand schemes shared by the split conv kernels (kernels_conv_split.hip,
+// kernels_resblock.hip): how an fp32 operand becomes 16-bit MFMA pieces, which piece products
+// are accumulated, and the f16x3 input scale from a producer's max-abs statistics.
+#pragma once
+
+#include "conv_device.hpp"
+
+namespace tts {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned short bf16_bits(__bf16 h) { return __builtin_bit_cast(unsigned short, h); }
+__device__ __forceinline__ unsigned short f16_bits(_Float16 h) { return __builtin_bit_cast(unsigned short, h); }
+
+struct SchemeX6 {
+  static constexpr int NP = 3;        // pieces per operand
+  static constexpr int ROWB = 112;    // LDS bytes per staged row (3 x 32 B + 16 B pad)
+  static constexpr int NACC = 1;      // accumulators per output block
+  static constexpr int NPROD = 6;     // products per step, smallest first
+  static constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+  static constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+  static constexpr int PACC[6] = {0, 0, 0, 0, 0, 0};
+  static constexpr bool SCALED = false;
+  // x = p0 + p1 + p2 exactly (round-to-nearest-even at every piece)
+  __device__ static __forceinline__ void split(float x, unsigned short (&p)[3]) {
+    const __bf16 a0 = (__bf16)x;
+    const float r1 = x - (float)a0;
+    const __bf16 a1 = (__bf16)r1;
+    const float r2 = r1 - (float)a1;
+    p[0] = bf16_bits(a0);
+    p[1] = bf16_bits(a1);
+    p[2] = bf16_bits((__bf16)r2);
+  }
+  __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
+struct SchemeH3 {
+  static constexpr int NP = 2;
+  static constexpr int ROWB = 80;     // 2 x 32 B + 16 B pad
+  static constexpr int NACC = 1;
+  static constexpr int NPROD = 3;     // lo*hi, hi*lo, hi*hi
+  static constexpr int PA[3] = {1, 0, 0};
+  static constexpr int PB[3] = {0, 1, 0};
+  static constexpr int PACC[3] = {0, 0, 0};
+  static constexpr bool SCALED = true;
+  // x (already scaled into [0, 2^14]) = hi + lo to 22 bits
+  __device__ static __forceinline__ void split(float x, unsigned short (&p)[2]) {
+    const _Float16 h = (_Float16)x;
+    p[0] = f16_bits(h);
+    p[1] = f16_bits((_Float16)(x - (float)h));
+  }
+  __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+// Plain bf16 (MATH_BF16): one bf16 piece per operand, one product, fp32 accumulation.
+struct SchemeB1 {
+  static constexpr int NP = 1;
+  static constexpr int ROWB = 48;     // 32 B + 16 B pad (conflict-free like the other pitches)
+  static constexpr int NACC = 1;
+  static constexpr int NPROD = 1;
+  static constexpr int PA[1] = {0};
+  static constexpr int PB[1] = {0};
+  static constexpr int PACC[1] = {0};
+  static constexpr bool SCALED = false;
+  __device__ static __forceinline__ void split(float x, unsigned short (&p)[1]) { p[0] = bf16_bits((__bf16)x); }
+  __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
+// Exponent e such that max|x| * 2^-e lies in [2^13, 2^14): read the 64 max-abs slots the
+// producer published (one per lane), wave max, frexp.  No statistics, zero or non-finite max:
+// e = 0 (an overflowing input then yields inf, as fp16 would; NaN propagates).
+__device__ __forceinline__ int amax_exp(const unsigned* slots, int b) {
+  if (!slots) return 0;
+  float m = __uint_as_float(slots[(size_t)b * 64 + (threadIdx.x & 63)]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  int e = 0;
+  if (m > 0.f && m < INFINITY) {
+    int E;
+    (void)frexpf(m, &E);
+    e = E - 14;
+  }
+  return __builtin_amdgcn_readfirstlane(e);
+}
+
+}  // namespace tts

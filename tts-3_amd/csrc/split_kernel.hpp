@@ -1,0 +1,269 @@
+// The split-precision conv1d kernel template and its launch dispatch over (K, tile), shared by
+// the per-scheme translation units kernels_conv_split_{x6,h3,b1}.hip (compiled in parallel).
+// See kernels_conv_split.hip for the algorithm, the tile table and the selection.
+#pragma once
+
+#include "split_device.hpp"
+
+namespace tts {
+
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
+struct SplitCfg {
+  static constexpr int WM = BM / (32 * TM);
+  static constexpr int WN = BN / (32 * TN);
+  static constexpr int CK = 16 * G;
+  static constexpr int XROWS = BN + HMAX;
+  static constexpr int XSZB = G * XROWS * S::ROWB;  // bytes per LDS buffer
+  static constexpr int UNITS = G * XROWS * 4;       // staging units (group, row, channel quad)
+  static constexpr int UPT = (UNITS + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(XSZB % 16 == 0, "");
+};
+
+#ifndef X6_ABLATE
+#define X6_ABLATE 0  // ablation builds (scripts/gpu_ablate.sh): 1 no staging refill, 2 no A stream
+#endif
+
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
+__global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
+  using C = SplitCfg<S, K, BM, BN, TM, TN, G, HMAX, PD>;
+  constexpr int NP = S::NP;
+  constexpr bool H3 = S::SCALED;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / C::WN;
+  const int wn = wave % C::WN;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+
+  const int t0 = blockIdx.x * BN;
+  const int mt = blockIdx.y;
+  const int b = blockIdx.z;
+  const int d = a.dil;
+  const int XW = BN + (K - 1) * d;
+  const int Tin = a.Tin;
+  const int Tout = a.Tout;
+  const int Cin = a.Cin;
+  const int nc = a.n_chunks;
+  const int ex = H3 ? amax_exp(a.amax_in, b) : 0;
+  const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;  // exact power of two
+
+  // x of batch item b; one buffer descriptor per chunk (scalar ops), every range-checked
+  // offset in the per-lane voffset: zero rows and channels >= Cin read 0 through the hardware
+  // range check instead of per-element selects
+  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  const unsigned chb = (unsigned)Tin * 4u;  // bytes per channel row
+
+  // staging units (chunk invariant): unit u -> channel quad q, row r, group g
+  unsigned uvoff[C::UPT];  // byte offset of channel (16g+4q) at the clamped source time, or OOB
+  int ulds[C::UPT];        // LDS offset of the row's quad
+#pragma unroll
+  for (int i = 0; i < C::UPT; ++i) {
+    const int u = tid + i * 256;
+    const int q = u & 3;
+    const int rr = u >> 2;
+    const int g = rr / XW;
+    const int r = rr - g * XW;
+    const int ts = t0 - a.pad + r;
+    // source frame ts - rep_pad, clamped (replicate) when rep_pad > 0, else zero outside [0, Tin)
+    const bool ok = (g < G) && ts >= 0 && ts < (a.rep_pad ? Tout : Tin);
+    int src = ts - a.rep_pad;
+    src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
+    uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
+    ulds[i] = (g < G) ? (g * C::XROWS + r) * S::ROWB + 8 * q : -1;
+  }
+
+  f32x4 xreg[C::UPT];
+  auto load_x = [&](int c) {
+    const int c0 = c * C::CK;
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
+#pragma unroll
+    for (int i = 0; i < C::UPT; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
+    }
+  };
+  auto store_x = [&](int buf) {
+    unsigned char* xl = smem + buf * C::XSZB;
+    const float slope = a.in_slope;
+#pragma unroll
+    for (int i = 0; i < C::UPT; ++i) {
+      if (ulds[i] >= 0) {
+        u16x4 pv[NP];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned short h[NP];
+          float v = lrelu2(xreg[i][j], slope);
+          if (H3) v *= xscale;
+          S::split(v, h);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(xl + ulds[i] + 32 * p) = pv[p];
+      }
+    }
+  };
+
+  // A streams: f32x4 units, fragment (mb, step s, piece p) at ((mb*S + s)*NP + p)*64 + lane
+  // (descriptor per m-block from wave-uniform values, step/piece offsets in the scalar soffset)
+  rsrc_t ra[TM];
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const int mb = mt * (BM / 32) + wmu * TM + m;
+    ra[m] = make_rsrc(a.w + ((size_t)mb * nc * G * K) * (NP * 256), 0xFFFFFFFFu);
+  }
+  const unsigned avoff = (unsigned)lane * 16u;
+
+  f32x16 acc[S::NACC][TM][TN];
+#pragma unroll
+  for (int h = 0; h < S::NACC; ++h)
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[h][m][n] = f32x16{};
+
+  const int xrow0 = wn * TN * 32 + l32;
+
+  f32x4 ar[PD + 1][TM][NP], bcur[TN][NP], bnext[TN][NP];
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
+
+  auto read_b = [&](const unsigned char* xl, int g, int k, f32x4 (*dst)[NP]) {
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int r = xrow0 + n * 32 + k * d;
+      const unsigned char* p = xl + (g * C::XROWS + r) * S::ROWB + 16 * half;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
+    }
+  };
+
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+
+  for (int c = 0; c < nc; ++c) {
+    const int buf = c & 1;
+    const unsigned char* xl = smem + buf * C::XSZB;
+    const bool more = c + 1 < nc;
+    if ((X6_ABLATE & 1) == 0 && more) load_x(c + 1);
+    read_b(xl, 0, 0, bcur);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int s = (c * G + g) * K + k;
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            ar[PD][m][q] = (X6_ABLATE & 2) ? ar[0][m][q] : bload4(ra[m], avoff, (unsigned)((s + PD) * NP + q) * 1024u);
+        const bool bnext_here = (k + 1 < K) || (g + 1 < G);
+        if (bnext_here) read_b(xl, (k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
+        // keep the prefetches ahead of this step's MFMAs (the scheduler otherwise sinks them
+        // to their use and exposes the L2 / LDS latency every step)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int n = 0; n < TN; ++n)
+              acc[S::PACC[e]][m][n] = S::mfma(ar[0][m][S::PA[e]], bcur[n][S::PB[e]], acc[S::PACC[e]][m][n]);
+#pragma unroll
+        for (int p = 0; p < PD; ++p)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
+        if (bnext_here) {
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+        }
+      }
+    }
+    if ((X6_ABLATE & 1) == 0 && more) store_x(buf ^ 1);
+    __syncthreads();
+  }
+
+  if constexpr (H3) {
+    const float sc = ldexpf(1.f, ex + a.w_exp);  // undo both scalings (exact)
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[0][m][n] *= sc;
+  }
+  if constexpr (K == 2) {
+    convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+  } else {
+    conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+  }
+}
+
+namespace split_detail {
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE>
+void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
+  dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
+  const int halo = (K - 1) * a.dil;
+  if (halo <= (K - 1) * 5) {
+    hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD>), grid, dim3(256), 0, s, a);
+  } else if (WIDE && halo <= 96) {
+    hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, WIDE ? 96 : 0, PD>), grid, dim3(256), 0, s, a);
+  } else {
+    throw Error(3, "conv1d(split): (kernel_size-1)*dilation = " + std::to_string(halo) + " too large for this tile");
+  }
+}
+
+template <class S, int K>
+void launch_split_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
+  switch (tile) {
+    case 0: launch_split_t<S, K, 128, 128, 2, 2, 1, 1, true>(a, B, s); break;
+    case 1: launch_split_t<S, K, 64, 256, 2, 2, 1, 1, true>(a, B, s); break;
+    case 2: launch_split_t<S, K, 32, 512, 1, 4, 1, 1, true>(a, B, s); break;
+    case 3: launch_split_t<S, K, 128, 128, 2, 2, 2, 1, false>(a, B, s); break;
+    case 4: launch_split_t<S, K, 64, 128, 2, 1, 2, 1, false>(a, B, s); break;
+    case 5: launch_split_t<S, K, 32, 256, 1, 2, 2, 1, false>(a, B, s); break;
+    case 6: launch_split_t<S, K, 64, 256, 2, 2, 2, 1, false>(a, B, s); break;
+    case 7: launch_split_t<S, K, 128, 128, 2, 2, 1, 2, false>(a, B, s); break;
+    case 8: launch_split_t<S, K, 64, 128, 2, 1, 2, 2, false>(a, B, s); break;
+    case 9: launch_split_t<S, K, 64, 256, 2, 2, 2, 2, false>(a, B, s); break;
+    case 10: launch_split_t<S, K, 64, 256, 2, 2, 1, 2, false>(a, B, s); break;
+    case 11: launch_split_t<S, K, 32, 256, 1, 2, 2, 2, false>(a, B, s); break;
+    case 12: launch_split_t<S, K, 64, 128, 2, 1, 2, 3, false>(a, B, s); break;
+    case 13: launch_split_t<S, K, 128, 128, 2, 2, 2, 2, false>(a, B, s); break;
+    case 14: launch_split_t<S, K, 32, 256, 1, 2, 1, 1, false>(a, B, s); break;
+    case 15: launch_split_t<S, K, 32, 256, 1, 2, 1, 2, false>(a, B, s); break;
+    case 16: launch_split_t<S, K, 32, 128, 1, 1, 1, 2, false>(a, B, s); break;
+    case 17: launch_split_t<S, K, 64, 128, 2, 1, 1, 1, false>(a, B, s); break;
+    case 18: launch_split_t<S, K, 64, 128, 2, 1, 1, 2, false>(a, B, s); break;
+    case 19: launch_split_t<S, K, 32, 512, 1, 4, 1, 2, false>(a, B, s); break;
+    default: throw Error(3, "conv1d(split): bad tile index " + std::to_string(tile));
+  }
+}
+
+template <class S>
+void launch_split_s(const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  switch (K) {
+    case 1: launch_split_k<S, 1>(a, B, tile, s); break;
+    case 2: launch_split_k<S, 2>(a, B, tile, s); break;  // ConvTranspose1d (Conv1dArgs::ups)
+    case 3: launch_split_k<S, 3>(a, B, tile, s); break;
+    case 5: launch_split_k<S, 5>(a, B, tile, s); break;
+    case 7: launch_split_k<S, 7>(a, B, tile, s); break;
+    case 11: launch_split_k<S, 11>(a, B, tile, s); break;
+    default: throw Error(3, "conv1d(split): kernel size " + std::to_string(K) + " not supported (1,3,5,7,11)");
+  }
+}
+}  // namespace split_detail
+
+}  // namespace tts
