@@ -271,6 +271,8 @@ def main():
 
     # dominant-kernel roofline from one profiled forward (hipEvents per launch)
     _, rows = g.profile(mel)
+    if os.environ.get("TTS_FORWARD_NAMES") and rank == 0:  # launch sequence for scripts/traffic_from_pmc.py
+        json.dump([r["name"] for r in rows], open(os.environ["TTS_FORWARD_NAMES"], "w"))
     fam_name, fam, fams = dominant_kernel(rows)
     per_launch_flops = fam["flops"] / fam["n"]
     avg_ms = fam["ms"] / fam["n"]

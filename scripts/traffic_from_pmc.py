@@ -4,7 +4,8 @@
 Input: the directory written by scripts/profile_round.sh (a kernel trace, a FETCH_SIZE pass and
 a WRITE_SIZE pass over `bench.py --steps S --warmup W --no-alt --no-glow --no-cpu-baseline`).
 Every forward enqueues the same launch sequence (HifiganGenerator executor order), so the
-library's dispatches are cut into forwards and named by position.
+library's dispatches are cut into forwards and named by position; the names come from the
+profiled forward bench.py dumps (TTS_FORWARD_NAMES=<root>/forward_names.json).
 
 Counter handling (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE and WRITE_SIZE are
 KiB counters, collected in separate passes.  The gfx950 FETCH_SIZE undercount is documented for
@@ -64,7 +65,8 @@ def main():
     mode = sys.argv[2] if len(sys.argv) > 2 else "f16x3"
     B, T = 32, 1024
     out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/traffic_hifigan_r01.json"
-    names = forward_names(mode)
+    fn = os.path.join(root, "forward_names.json")
+    names = json.load(open(fn)) if os.path.exists(fn) else forward_names(mode)
     per = {}
     for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         seq = [(n, v) for n, v in read_pmc(find(os.path.join(root, sub), "counter_collection.csv"), counter) if ours(n)]
