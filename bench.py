@@ -66,6 +66,7 @@ def parse():
                    help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
     p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
     p.add_argument("--no-glow", action="store_true", help="skip the Glow-TTS decoder measurement")
+    p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -233,6 +234,68 @@ def glow_bench(dev, math_mode, steps=10, warmup=3, B=16, T=768, cpu=True):
     return out
 
 
+def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
+    """Config 3: Glow-TTS (LJSpeech cfg) + HiFiGAN-v1 end to end, token ids -> waveform, B = 16 x 128
+    tokens (durations ~6 frames/token from the synthetic predictor -> ~768 mel frames).
+    ``modes`` = (glow decoder mode, vocoder mode) per variant; the encoder always runs exact fp32
+    (its durations are ceil()-quantised, so they must match the reference's)."""
+    from tts_amd import synthetic
+    from tts_amd.config import GLOW_TTS_DECODER as G, GLOW_TTS_ENCODER as E
+    from tts_amd.tts import GlowTTS
+
+    ecfg = dict(E, num_chars=64)
+    dcfg = dict(in_channels=G["in_channels"], hidden_channels=G["hidden_channels"], kernel_size=G["kernel_size"],
+                dilation_rate=G["dilation_rate"], num_flow_blocks=G["num_flow_blocks"],
+                num_coupling_layers=G["num_coupling_layers"], num_splits=G["num_splits"],
+                num_squeeze=G["num_squeeze"])
+    sd = {f"encoder.{k}": v for k, v in
+          synthetic.glow_encoder_state_dict(**ecfg, seed=8642, log_duration=1.872).items()}
+    sd.update({f"decoder.{k}": v for k, v in synthetic.glow_decoder_state_dict(**dcfg, seed=4321).items()})
+    tok = synthetic.tokens(B, T_x, 64, seed=11).to(dev)
+    lens = torch.full((B,), T_x, dtype=torch.int64, device=dev)
+    out = {"workload": f"Glow-TTS LJSpeech cfg + HiFiGAN-v1, [{B} x {T_x}] token ids -> waveform "
+                       "(encoder fp32, noise_scale 0, length_scale 1)", "variants": {}}
+    for label, (dmode, vmode) in modes.items():
+        m = GlowTTS(dict(num_chars=64), decoder_math_mode=dmode)
+        m.load_state_dict(sd)
+        m.eval()
+        m.store_inverse()
+        m = m.to(dev)
+        voc = build_generator(vmode, dev)
+
+        def step():
+            mel = m.inference(tok, {"x_lengths": lens})["model_outputs"].transpose(1, 2)
+            return voc.inference(mel)
+
+        for _ in range(warmup):
+            wav = step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            wav = step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        samples = wav.numel()
+        mel = m.inference(tok, {"x_lengths": lens})["model_outputs"].transpose(1, 2).contiguous()
+        torch.cuda.synchronize(dev)
+        e0 = time.perf_counter()
+        for _ in range(steps):
+            m.inference(tok, {"x_lengths": lens})
+        torch.cuda.synchronize(dev)
+        ms_glow = (time.perf_counter() - e0) / steps * 1e3
+        _, erows = m.encoder.profile(tok, lens)
+        out["mel_frames"] = int(mel.shape[2])
+        out["variants"][label] = {
+            "glow_decoder_math_mode": dmode, "vocoder_math_mode": vmode,
+            "ms_per_step": ms, "samples_per_s": samples / (ms / 1e3),
+            "rtf": (ms / 1e3) / (samples / SAMPLE_RATE),
+            "glow_tts_inference_ms": ms_glow,
+            "encoder_kernel_ms": sum(r["ms"] for r in erows), "encoder_launches": len(erows),
+        }
+        del m, voc
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -321,6 +384,10 @@ def main():
         glow_mode = "fp32x6" if a.math_mode == "f16x3" else a.math_mode  # bf16 runs as is
         glow = glow_bench(dev, glow_mode, cpu=(world == 1 and not a.no_cpu_baseline))
 
+    e2e = None
+    if rank == 0 and world == 1 and not a.no_e2e:
+        e2e = glow_tts_e2e_bench(dev, {"fp32_faithful": ("fp32x6", "f16x3"), "bf16": ("bf16", "bf16")})
+
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -364,6 +431,7 @@ def main():
             "cpu_baseline": cpu,
             "alt_math_mode": alt,
             "glow_decoder": glow,
+            "glow_tts_e2e": e2e,
             "accuracy_vs_fp64_oracle": acc,
         }
         if comm:

@@ -13,6 +13,12 @@
  *       Decoder.__init__                 :68-111    -> tts_glow_decoder_create
  *       Decoder.forward(reverse=True)    :113-137   -> tts_glow_decoder_forward
  *       Decoder.store_inverse            :139-141   (W^-1 arrives precomputed)
+ *   Glow-TTS encoder   TTS/tts/layers/glow_tts/encoder.py (rel_pos_transformer)
+ *       Encoder.__init__                 :83-141    -> tts_glow_encoder_create
+ *       Encoder.forward                  :143-179   -> tts_glow_encoder_forward
+ *   Glow-TTS inference glue  TTS/tts/models/glow_tts.py
+ *       GlowTTS.inference durations      :349-351   -> tts_glow_durations
+ *       generate_path + compute_outputs + z :352-361 -> tts_glow_expand
  *
  * The reference has no native FFI for this path (it is pure Python over ATen); the Python
  * binding a maintainer adds is the ctypes stub in INTEGRATION.md.
@@ -186,6 +192,76 @@ int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask
 int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, int B, int C,
                                       int T, int reverse, float* d_y, void* hip_stream,
                                       TtsLaunchRecord* records, int max_records, int* n_records);
+
+/* ------------------------------------------------------------------------------------ */
+/* Glow-TTS encoder (rel_pos_transformer) and the GlowTTS.inference glue                   */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors Encoder.__init__ (encoder.py:83-141) for encoder_type "rel_pos_transformer", with the
+ * transformer's encoder_params flattened (transformer.py:345-357; GlowTTS passes
+ * in = out = hidden = hidden_channels_enc). */
+typedef struct TtsGlowEncoderCfg {
+  int num_chars;            /* embedding rows */
+  int out_channels;         /* 80 (mel channels) */
+  int hidden_channels;      /* 192 (hidden_channels_enc) */
+  int hidden_channels_dp;   /* 256 */
+  int hidden_channels_ffn;  /* 768 (encoder_params) */
+  int num_heads;            /* 2 */
+  int num_layers;           /* 6 */
+  int kernel_size;          /* 3: FFN conv kernel (encoder_params) */
+  int rel_attn_window_size; /* 0 = None (Glow-TTS default); 4 in the VITS-style encoders */
+  int mean_only;            /* 1 (GlowTTSConfig default): x_logs = zeros */
+  int use_prenet;           /* 1: ResidualConv1dLayerNormBlock(k5, 3 layers) before the transformer */
+  int c_in_channels;        /* 0 (speaker-conditioned duration predictor not implemented: must be 0) */
+  int math_mode;            /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
+} TtsGlowEncoderCfg;
+
+/* Host weight order (R = 2*rel_attn_window_size + 1, dk = hidden/num_heads, H = hidden):
+ *   emb.weight [num_chars][H]
+ *   if use_prenet: for l < 3: prenet.conv_layers.l.weight [H][H][5], bias [H],
+ *                             prenet.norm_layers.l.gamma [H], beta [H]
+ *                  prenet.proj.weight [H][H][1], bias [H]
+ *   for l < num_layers (encoder.*):
+ *       attn_layers.l.conv_q.weight [H][H][1], bias, conv_k.*, conv_v.*, conv_o.*
+ *       if rel_attn_window_size: attn_layers.l.emb_rel_k [1][R][dk], emb_rel_v [1][R][dk]
+ *       norm_layers_1.l.gamma [H], beta [H]
+ *       ffn_layers.l.conv_1.weight [ffn][H][k], bias [ffn], conv_2.weight [H][ffn][k], bias [H]
+ *       norm_layers_2.l.gamma [H], beta [H]
+ *   proj_m.weight [out][H][1], bias [out];  if !mean_only: proj_s.weight, bias
+ *   duration_predictor.conv_1.weight [dp][H][3], bias, norm_1.gamma, beta,
+ *                      conv_2.weight [dp][dp][3], bias, norm_2.gamma, beta,
+ *                      proj.weight [1][dp][1], proj.bias [1] */
+int tts_glow_encoder_num_weights(const TtsGlowEncoderCfg* cfg);
+int64_t tts_glow_encoder_weight_numel(const TtsGlowEncoderCfg* cfg, int idx);
+int tts_glow_encoder_create(const TtsGlowEncoderCfg* cfg, const float* const* host_weights, int device,
+                            void** handle);
+int tts_glow_encoder_destroy(void* handle);
+/* (x_m, x_logs, logw, x_mask) = Encoder.forward(tokens, lengths): tokens [B][T] int64 (ids in
+ * [0, num_chars); padded positions may hold any id), lengths [B] int64; outputs x_m, x_logs
+ * [B][out][T], logw [B][1][T], x_mask [B][1][T].  x_logs may be NULL when mean_only.  T <= 3072. */
+int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
+                             float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask, void* hip_stream);
+int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
+                                      int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+                                      void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                      int* n_records);
+
+/* glow_tts.py:350-352 and :147: w_ceil[B][1][T_x] = max(ceil((exp(logw) - 1) * x_mask *
+ * length_scale), 1); y_lengths[B] (int64) = max(sum(w_ceil), 1); o_attn_dur [B][1][T_x] =
+ * log(1 + sum_j attn[i][j]) * x_mask (may be NULL).  The caller reads y_lengths back to size
+ * T_y = max(y_lengths) (the reference's sequence_mask(y_lengths, None), glow_tts.py:353). */
+int tts_glow_durations(const float* d_logw, const float* d_x_mask, int B, int T_x, float length_scale,
+                       float* d_w_ceil, int64_t* d_y_lengths, float* d_o_attn_dur, void* hip_stream);
+/* glow_tts.py:353-361: y_mask [B][1][T_y]; attn = generate_path(w_ceil, x_mask*y_mask)
+ * (helpers.py:154-169); y_mean = attn^T o_mean, y_log_scale = attn^T o_log_scale (compute_outputs
+ * :138-145); z = (y_mean + exp(y_log_scale) * noise * noise_scale) * y_mask.
+ * o_log_scale NULL = zeros (mean_only); noise [B][C][T_y] (torch.randn_like drawn by the caller)
+ * NULL = zeros.  y_mean, y_log_scale [B][C][T_y] and attn [B][T_x][T_y] may be NULL.
+ * T_y must be >= max(y_lengths).  T_x <= 16384. */
+int tts_glow_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t* d_y_lengths,
+                    const float* d_o_mean, const float* d_o_log_scale, const float* d_noise, float noise_scale,
+                    int B, int C, int T_x, int T_y, float* d_z, float* d_y_mask, float* d_y_mean,
+                    float* d_y_log_scale, float* d_attn, void* hip_stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* VITS flow: ResidualCouplingBlocks, reverse (TTS/tts/layers/vits/networks.py:169-232)     */

@@ -3,6 +3,7 @@
 Run in the development container only (it imports /root/reference, which does not exist on
 the GPU box):   python tests/golden/make_goldens.py        (HiFiGAN + Glow fixtures)
                 python tests/golden/make_goldens.py vits   (VITS flow fixtures)
+                python tests/golden/make_goldens.py glow_tts (Glow-TTS encoder + inference glue)
 
 Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
 but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
@@ -56,6 +57,103 @@ def import_reference_vits_flow():
     from TTS.tts.layers.vits.networks import ResidualCouplingBlocks
 
     return ResidualCouplingBlocks
+
+
+def import_reference_glow_tts():
+    import_reference()
+    from TTS.tts.layers.glow_tts.decoder import Decoder
+    from TTS.tts.layers.glow_tts.encoder import Encoder
+    from TTS.tts.utils.helpers import generate_path, sequence_mask
+
+    return Encoder, Decoder, generate_path, sequence_mask
+
+
+def _ref_encoder(Encoder, cfg, seed):
+    torch.manual_seed(0)
+    ref = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
+                  "rel_pos_transformer", dict(cfg["encoder_params"]), dropout_p_dp=0.1,
+                  mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"], c_in_channels=0)
+    sd = synthetic.glow_encoder_state_dict(**cfg, seed=seed)
+    ref.load_state_dict(sd)
+    ref.eval()
+    return ref
+
+
+def glow_encoder_case(Encoder, name, cfg, seed, B, T, lengths, tok_seed):
+    ref = _ref_encoder(Encoder, cfg, seed)
+    tok = synthetic.tokens(B, T, cfg["num_chars"], seed=tok_seed)
+    lens = torch.tensor(lengths)
+    with torch.no_grad():
+        o32 = ref(tok, lens)
+        o64 = ref.double()(tok, lens)
+    names = ["x_m", "x_logs", "logw", "x_mask"]
+    arrays = dict(tokens=tok.numpy(), lengths=lens.numpy())
+    for n, a, b in zip(names, o32, o64):
+        arrays[f"{n}_ref_fp32"] = a.float().numpy()
+        arrays[f"{n}_ref_fp64"] = b.numpy()
+    meta = dict(kind="glow_encoder", config=cfg, seed=seed, tok_seed=tok_seed, B=B, T=T, lengths=lengths)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: x_m std {o32[0].std():.3f} logw mean {o32[2].sum() / o32[3].sum():.3f} "
+          f"max|fp32-fp64| x_m {np.abs(arrays['x_m_ref_fp32'] - arrays['x_m_ref_fp64']).max():.2e}")
+
+
+def glow_tts_case(Encoder, Decoder, generate_path, sequence_mask, name, ecfg, dcfg, eseed, dseed, B, T, lengths,
+                  tok_seed, noise_scale, length_scale):
+    """Tokens -> Encoder -> GlowTTS.inference glue (glow_tts.py:349-363) -> Decoder reverse, fp32 and
+    fp64.  GlowTTS itself imports coqpit/trainer (absent), so the glue's 12 lines are restated here
+    around the reference's own generate_path / sequence_mask; the noise is drawn here and stored."""
+    enc = _ref_encoder(Encoder, ecfg, eseed)
+    torch.manual_seed(0)
+    dec = Decoder(dcfg["in_channels"], dcfg["hidden_channels"], dcfg["kernel_size"], dcfg["dilation_rate"],
+                  dcfg["num_flow_blocks"], dcfg["num_coupling_layers"], dropout_p=0.05,
+                  num_splits=dcfg["num_splits"], num_squeeze=dcfg["num_squeeze"], sigmoid_scale=False,
+                  c_in_channels=0)
+    dec.load_state_dict(synthetic.glow_decoder_state_dict(**dcfg, seed=dseed))
+    dec.eval()
+    dec.store_inverse()
+    tok = synthetic.tokens(B, T, ecfg["num_chars"], seed=tok_seed)
+    lens = torch.tensor(lengths)
+    arrays = dict(tokens=tok.numpy(), lengths=lens.numpy())
+
+    def infer(e, d, dtype, noise):
+        with torch.no_grad():
+            o_mean, o_log_scale, o_dur_log, x_mask = e(tok, lens)
+            w = (torch.exp(o_dur_log) - 1) * x_mask * length_scale
+            w_ceil = torch.clamp_min(torch.ceil(w), 1)
+            y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
+            y_mask = torch.unsqueeze(sequence_mask(y_lengths, None), 1).to(x_mask.dtype)
+            attn_mask = torch.unsqueeze(x_mask, -1) * torch.unsqueeze(y_mask, 2)
+            attn = generate_path(w_ceil.squeeze(1), attn_mask.squeeze(1)).unsqueeze(1)
+            y_mean = torch.matmul(attn.squeeze(1).transpose(1, 2), o_mean.transpose(1, 2)).transpose(1, 2)
+            y_log_scale = torch.matmul(attn.squeeze(1).transpose(1, 2), o_log_scale.transpose(1, 2)).transpose(1, 2)
+            o_attn_dur = torch.log(1 + torch.sum(attn, -1)) * x_mask
+            if noise is None:
+                noise = torch.randn(y_mean.shape, generator=torch.Generator().manual_seed(tok_seed + 100))
+            z = (y_mean + torch.exp(y_log_scale) * noise.to(dtype) * noise_scale) * y_mask
+            y, _ = d(z, y_mask, reverse=True)
+        out = dict(x_m=o_mean, logw=o_dur_log, x_mask=x_mask, w=w, w_ceil=w_ceil, y_lengths=y_lengths,
+                   y_mask=y_mask, attn=attn.squeeze(1), y_mean=y_mean, o_attn_dur=o_attn_dur, z=z, mel=y)
+        return out, noise
+
+    o32, noise = infer(enc, dec, torch.float32, None)
+    o64, _ = infer(enc.double(), dec.double(), torch.float64, noise)
+    for k in ("w_ceil", "y_lengths"):
+        assert torch.equal(o32[k].double(), o64[k].double()), f"{k}: fp32 and fp64 reference disagree"
+    arrays["noise"] = noise.numpy()
+    for k, v in o32.items():
+        arrays[f"{k}_ref_fp32"] = v.numpy()
+    for k, v in o64.items():
+        arrays[f"{k}_ref_fp64"] = v.numpy()
+    wv = o64["w"][o64["x_mask"] > 0]
+    frac = (wv - torch.floor(wv)).numpy()
+    margin = float(np.minimum(frac, 1 - frac).min())
+    meta = dict(kind="glow_tts", encoder=ecfg, decoder=dcfg, eseed=eseed, dseed=dseed, tok_seed=tok_seed, B=B, T=T,
+                lengths=lengths, noise_scale=noise_scale, length_scale=length_scale, ceil_margin=margin)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: y_lengths {o32['y_lengths'].tolist()} mel {tuple(o32['mel'].shape)} "
+          f"ceil margin {margin:.2e} max|fp32-fp64| mel {np.abs(arrays['mel_ref_fp32'] - arrays['mel_ref_fp64']).max():.2e}")
 
 
 def hifigan_case(HifiganGenerator, name, cfg, seed, B, T, mel_seed, stage_B=None, stage_T=None, with_forward=True):
@@ -176,6 +274,8 @@ def vits_flow_case(ResidualCouplingBlocks, name, cfg, seed, B, T, lengths, x_see
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "vits":
         return main_vits()
+    if len(sys.argv) > 1 and sys.argv[1] == "glow_tts":
+        return main_glow_tts()
     HifiganGenerator, Decoder = import_reference()
     v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
@@ -215,6 +315,24 @@ def main_vits():
     vits_flow_case(ResidualCouplingBlocks, "vits_flow_b2_t40", flow, seed=2468, B=2, T=40, lengths=[40, 27], x_seed=31)
     vits_flow_case(ResidualCouplingBlocks, "vits_flow_cond_b3_t17", dict(flow, cond_channels=8), seed=2469, B=3,
                    T=17, lengths=[17, 9, 1], x_seed=32)
+
+
+def main_glow_tts():
+    Encoder, Decoder, generate_path, sequence_mask = import_reference_glow_tts()
+    from tts_amd.config import GLOW_TTS_ENCODER
+
+    # G6: LJSpeech Glow-TTS (glow_tts_config.py defaults), tokens -> mel through encoder, glue and decoder
+    ecfg = dict(GLOW_TTS_ENCODER, num_chars=64)
+    dcfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+                num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    glow_tts_case(Encoder, Decoder, generate_path, sequence_mask, "glow_tts_b3_t23", ecfg, dcfg, eseed=8642,
+                  dseed=4321, B=3, T=23, lengths=[23, 17, 1], tok_seed=41, noise_scale=0.33, length_scale=1.0)
+    # G7: encoder variant: relative attention window 4 (VITS text encoder style), proj_s, no prenet
+    rcfg = dict(num_chars=40, out_channels=24, hidden_channels=96, hidden_channels_dp=64,
+                encoder_params={"kernel_size": 3, "dropout_p": 0.1, "num_layers": 2, "num_heads": 2,
+                                "hidden_channels_ffn": 192, "rel_attn_window_size": 4},
+                mean_only=False, use_prenet=False)
+    glow_encoder_case(Encoder, "glow_encoder_rel_b2_t19", rcfg, seed=97, B=2, T=19, lengths=[19, 11], tok_seed=43)
 
 
 if __name__ == "__main__":

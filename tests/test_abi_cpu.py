@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 105
+    assert N.lib().tts_abi_version() == 106
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -185,3 +185,87 @@ def test_null_arguments_return_invalid():
     assert b"NULL" in lib.tts_last_error()
     assert lib.tts_hifigan_destroy(None) == N.TTS_OK
     assert lib.tts_glow_decoder_destroy(None) == N.TTS_OK
+
+
+# ------------------------------------------------------------------------ Glow-TTS encoder / glue
+def _glow_tts_cfg(**over):
+    from tts_amd.config import GLOW_TTS_ENCODER
+
+    return dict(GLOW_TTS_ENCODER, num_chars=64, **over)
+
+
+def test_glow_encoder_weight_inventory_matches_reference_state_dict():
+    from tts_amd.tts import Encoder
+
+    cfg = _glow_tts_cfg()
+    sd = synthetic.glow_encoder_state_dict(**cfg, seed=1)
+    e = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
+                cfg["encoder_type"], cfg["encoder_params"], mean_only=True, use_prenet=True)
+    e.load_state_dict(sd)  # strict: the reference's key set
+    ws = e._weight_list()
+    n = N.lib().tts_glow_encoder_num_weights(ctypes.byref(e._cfg))
+    assert n == len(ws) == 1 + 14 + 6 * 16 + 2 + 10
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_encoder_weight_numel(ctypes.byref(e._cfg), i) == w.size
+    assert sum(w.size for w in ws) == sum(v.numel() for v in sd.values())
+
+
+def test_glow_encoder_rel_window_inventory():
+    from tts_amd.tts import Encoder
+
+    ep = {"kernel_size": 3, "dropout_p": 0.1, "num_layers": 2, "num_heads": 2, "hidden_channels_ffn": 192,
+          "rel_attn_window_size": 4}
+    sd = synthetic.glow_encoder_state_dict(num_chars=40, out_channels=24, hidden_channels=96, hidden_channels_dp=64,
+                                           encoder_params=ep, mean_only=False, use_prenet=False, seed=2)
+    e = Encoder(40, 24, 96, 64, "rel_pos_transformer", ep, mean_only=False, use_prenet=False)
+    e.load_state_dict(sd)
+    ws = e._weight_list()
+    assert len(ws) == N.lib().tts_glow_encoder_num_weights(ctypes.byref(e._cfg))
+    assert sum(w.size for w in ws) == sum(v.numel() for v in sd.values())
+
+
+def test_glow_encoder_c_validation_codes():
+    c = N.TtsGlowEncoderCfg(num_chars=10, out_channels=80, hidden_channels=192, hidden_channels_dp=256,
+                            hidden_channels_ffn=768, num_heads=5, num_layers=6, kernel_size=3)
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID  # transformer.py:75
+    assert b"num_heads" in N.lib().tts_last_error()
+    c.num_heads, c.c_in_channels = 2, 16
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c.c_in_channels, c.math_mode = 0, N.MATH_MODES["f16x3"]
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("over,code", [
+    (dict(encoder_params={"kernel_size": 9, "num_layers": 1, "num_heads": 2, "hidden_channels_ffn": 8}),
+     N.TTS_ERR_UNSUPPORTED),
+])
+def test_glow_encoder_config_validation(over, code):
+    from tts_amd.tts import Encoder
+
+    cfg = _glow_tts_cfg(**over)
+    with pytest.raises(N.NativeError) as e:
+        Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
+                cfg["encoder_type"], cfg["encoder_params"], mean_only=True)
+    assert e.value.code == code
+
+
+def test_glow_encoder_other_types_and_cpu_raise():
+    from tts_amd.tts import Encoder, GlowTTS
+
+    with pytest.raises(NotImplementedError):
+        Encoder(10, 80, 192, 256, "gated_conv", {"kernel_size": 5, "num_layers": 9})
+    m = GlowTTS(dict(num_chars=32))
+    with pytest.raises(RuntimeError, match="ROCm"):
+        m.inference(torch.zeros(1, 4, dtype=torch.long), {"x_lengths": torch.tensor([4])})
+
+
+def test_glow_tts_config_defaults_follow_reference():
+    from tts_amd.tts import GlowTTS
+
+    m = GlowTTS(dict(num_chars=32))
+    assert m.inference_noise_scale == 0.0 and m.length_scale == 1.0  # glow_tts_config.py:151-152
+    assert m.encoder.hidden_channels == 192 and m.encoder.hidden_channels_dp == 256
+    assert m.decoder.num_flow_blocks == 12 and m.decoder.hidden_channels == 192
+    keys = set(m.state_dict())
+    assert "encoder.encoder.attn_layers.5.conv_o.weight" in keys
+    assert "decoder.flows.35.wn.res_skip_layers.3.parametrizations.weight.original1" in keys

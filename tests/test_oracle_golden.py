@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from _util import goldens, max_abs, rel_rms
-from oracle import glow_ref, hifigan_ref, vits_ref
+from oracle import glow_ref, glow_tts_ref, hifigan_ref, vits_ref
 from tts_amd import synthetic
 
 HIFI = goldens("hifigan")
@@ -115,3 +115,54 @@ def test_synthetic_weights_deterministic():
         assert torch.equal(a[k], b[k])
     c = synthetic.hifigan_state_dict(seed=4)
     assert not torch.equal(a["conv_pre.bias"], c["conv_pre.bias"])
+
+
+GENC = goldens("glow_encoder")
+GTTS = goldens("glow_tts")
+
+
+def _enc_args(cfg):
+    return dict(hidden_channels=cfg["hidden_channels"], encoder_params=cfg["encoder_params"],
+                mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"])
+
+
+@pytest.mark.parametrize("name,meta,arr", GENC + [(n, dict(m, config=m["encoder"], seed=m["eseed"]), a)
+                                                   for n, m, a in GTTS],
+                         ids=[g[0] for g in GENC + GTTS])
+def test_glow_encoder_oracle_matches_reference(name, meta, arr):
+    cfg = meta["config"]
+    sd = synthetic.glow_encoder_state_dict(**cfg, seed=meta["seed"])
+    tok, lens = torch.from_numpy(arr["tokens"]), torch.from_numpy(arr["lengths"])
+    out = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float64, **_enc_args(cfg))
+    for n, o in zip(["x_m", "x_logs", "logw", "x_mask"], out):
+        if f"{n}_ref_fp64" in arr:
+            assert max_abs(o.numpy(), arr[f"{n}_ref_fp64"]) < 1e-10, n
+    out32 = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float32, **_enc_args(cfg))
+    assert max_abs(out32[0].numpy(), arr["x_m_ref_fp32"]) < 1e-5
+    assert max_abs(out32[2].numpy(), arr["logw_ref_fp32"]) < 1e-5
+
+
+@pytest.mark.parametrize("name,meta,arr", GTTS, ids=[g[0] for g in GTTS])
+def test_glow_tts_glue_oracle_matches_reference(name, meta, arr):
+    # durations -> path -> y_mean -> z from the reference's own fp64 encoder outputs
+    logw = torch.from_numpy(arr["logw_ref_fp64"])
+    xm = torch.from_numpy(arr["x_mask_ref_fp64"])
+    w_ceil, y_len = glow_tts_ref.durations(logw, xm, meta["length_scale"])
+    assert torch.equal(w_ceil, torch.from_numpy(arr["w_ceil_ref_fp64"]))
+    assert torch.equal(y_len, torch.from_numpy(arr["y_lengths_ref_fp64"]))
+    o_mean = torch.from_numpy(arr["x_m_ref_fp64"])
+    z, y_mask, y_mean, _, attn, dur = glow_tts_ref.expand(w_ceil, xm, y_len, o_mean, torch.zeros_like(o_mean),
+                                                          torch.from_numpy(arr["noise"]), meta["noise_scale"])
+    assert torch.equal(attn, torch.from_numpy(arr["attn_ref_fp64"]))
+    assert torch.equal(y_mask, torch.from_numpy(arr["y_mask_ref_fp64"]))
+    assert max_abs(y_mean.numpy(), arr["y_mean_ref_fp64"]) == 0.0
+    assert max_abs(dur.numpy(), arr["o_attn_dur_ref_fp64"]) < 1e-14
+    assert max_abs(z.numpy(), arr["z_ref_fp64"]) < 1e-14
+    # then the decoder oracle closes the chain to the reference's mel
+    dcfg = meta["decoder"]
+    dsd = synthetic.glow_decoder_state_dict(**dcfg, seed=meta["dseed"])
+    mel = glow_ref.glow_decoder_reverse(dsd, z, y_mask, dtype=torch.float64, **dcfg)
+    assert max_abs(mel.numpy(), arr["mel_ref_fp64"]) < 1e-10
+    # ceil() margin: no duration of the fixture sits within 1e-3 of an integer, so an fp32
+    # implementation that matches the encoder to ~1e-6 must reproduce w_ceil exactly
+    assert meta["ceil_margin"] > 1e-3

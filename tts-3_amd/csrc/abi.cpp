@@ -9,6 +9,7 @@
 
 #include "glow.hpp"
 #include "hifigan.hpp"
+#include "text.hpp"
 #include "vits.hpp"
 #include "tts_mi355x.h"
 
@@ -67,7 +68,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 105; }
+int tts_abi_version(void) { return 106; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -147,6 +148,97 @@ int tts_hifigan_forward_profiled(void* handle, const float* d_mel, int B, int C,
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);
+  });
+}
+
+// ----------------------------------------------------------------------------- Glow encoder + glue
+int tts_glow_encoder_num_weights(const TtsGlowEncoderCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::glow_encoder_validate(*cfg);
+    n = (int)tts::glow_encoder_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_glow_encoder_weight_numel(const TtsGlowEncoderCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::glow_encoder_validate(*cfg);
+    auto s = tts::glow_encoder_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_glow_encoder_create(const TtsGlowEncoderCfg* cfg, const float* const* host_weights, int device,
+                            void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::GlowEncoder(*cfg, host_weights, device);
+  });
+}
+
+int tts_glow_encoder_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::GlowEncoder*>(handle); });
+}
+
+int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
+                             float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::GlowEncoder*>(handle)->forward(d_tokens, d_lengths, B, T, d_x_m, d_x_logs, d_logw, d_x_mask,
+                                                    static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
+                                      int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+                                      void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                      int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::GlowEncoder*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->forward(d_tokens, d_lengths, B, T, d_x_m, d_x_logs, d_logw, d_x_mask, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+int tts_glow_durations(const float* d_logw, const float* d_x_mask, int B, int T_x, float length_scale,
+                       float* d_w_ceil, int64_t* d_y_lengths, float* d_o_attn_dur, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_logw && d_x_mask && d_w_ceil && d_y_lengths, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && T_x >= 1, 1, "batch and token count must be >= 1");
+    tts::launch_durations(d_logw, d_x_mask, d_w_ceil, d_y_lengths, d_o_attn_dur, B, T_x, length_scale,
+                          static_cast<hipStream_t>(hip_stream));
+    TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+int tts_glow_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t* d_y_lengths,
+                    const float* d_o_mean, const float* d_o_log_scale, const float* d_noise, float noise_scale,
+                    int B, int C, int T_x, int T_y, float* d_z, float* d_y_mask, float* d_y_mean,
+                    float* d_y_log_scale, float* d_attn, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_w_ceil && d_x_mask && d_y_lengths && d_o_mean && d_z && d_y_mask, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && C >= 1 && T_x >= 1 && T_y >= 1, 1, "bad expand shape");
+    tts::ExpandArgs a{};
+    a.w_ceil = d_w_ceil; a.x_mask = d_x_mask; a.y_len = d_y_lengths; a.o_mean = d_o_mean;
+    a.o_log_scale = d_o_log_scale; a.noise = d_noise; a.noise_scale = noise_scale;
+    a.C = C; a.T_x = T_x; a.T_y = T_y;
+    a.z = d_z; a.y_mask = d_y_mask; a.y_mean = d_y_mean; a.y_log_scale = d_y_log_scale; a.attn = d_attn;
+    tts::launch_expand(a, B, static_cast<hipStream_t>(hip_stream));
+    TTS_HIP_CHECK(hipGetLastError());
   });
 }
 

@@ -1,0 +1,269 @@
+// Glow-TTS Encoder (rel_pos_transformer) executor: every matmul of the reference runs on the
+// conv kernels (1x1 q|k|v as one 3H-row conv, conv_o with the residual fused, FFN k3 with the
+// relu and the mask fused, prenet k5, duration predictor k3), the rest on kernels_text.hip.
+// Reference: TTS/tts/layers/glow_tts/encoder.py:143-179, glow.py:55-67 (prenet),
+// transformer.py:117-201 (attention), :319-341 (FFN), :415-432 (layer loop),
+// duration_predictor.py:47-73, normalization.py:23-28.
+//
+// Masking: the reference masks conv INPUTS (x * x_mask); here every producer masks its output
+// instead (conv epilogue mask, LayerNorm * mask).  Padded positions never reach a valid one
+// (convs read masked planes, attention fills masked keys with -1e4) and every output the
+// encoder returns is multiplied by x_mask, so the returned tensors are the same.
+#include <cmath>
+#include <cstring>
+
+#include "text.hpp"
+
+namespace tts {
+
+namespace {
+int heads_dk(const TtsGlowEncoderCfg& c) { return c.hidden_channels / c.num_heads; }
+}  // namespace
+
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
+  std::vector<int64_t> n;
+  const int64_t H = c.hidden_channels, F = c.hidden_channels_ffn, K = c.kernel_size, D = c.hidden_channels_dp;
+  n.push_back((int64_t)c.num_chars * H);  // emb.weight
+  if (c.use_prenet) {
+    for (int l = 0; l < 3; ++l) {
+      n.push_back(H * H * 5); n.push_back(H);  // prenet.conv_layers.l
+      n.push_back(H); n.push_back(H);          // prenet.norm_layers.l gamma, beta
+    }
+    n.push_back(H * H); n.push_back(H);        // prenet.proj
+  }
+  for (int l = 0; l < c.num_layers; ++l) {
+    for (int j = 0; j < 4; ++j) { n.push_back(H * H); n.push_back(H); }  // conv_q, conv_k, conv_v, conv_o
+    if (c.rel_attn_window_size > 0) {
+      const int64_t R = 2 * c.rel_attn_window_size + 1;
+      n.push_back(R * heads_dk(c)); n.push_back(R * heads_dk(c));  // emb_rel_k, emb_rel_v
+    }
+    n.push_back(H); n.push_back(H);                          // norm_layers_1.l
+    n.push_back(F * H * K); n.push_back(F);                  // ffn_layers.l.conv_1
+    n.push_back(H * F * K); n.push_back(H);                  // ffn_layers.l.conv_2
+    n.push_back(H); n.push_back(H);                          // norm_layers_2.l
+  }
+  n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels);  // proj_m
+  if (!c.mean_only) { n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels); }  // proj_s
+  n.push_back(D * H * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_1, norm_1
+  n.push_back(D * D * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_2, norm_2
+  n.push_back(D); n.push_back(1);                                           // dp proj
+  return n;
+}
+
+void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
+  TTS_REQUIRE(c.num_chars >= 1 && c.out_channels >= 1 && c.hidden_channels >= 1 && c.hidden_channels_dp >= 1 &&
+                  c.hidden_channels_ffn >= 1 && c.num_layers >= 1,
+              1, "bad Glow encoder configuration");
+  TTS_REQUIRE(c.num_heads >= 1 && c.hidden_channels % c.num_heads == 0, 1,
+              "channels should be divisible by num_heads (transformer.py:75)");
+  TTS_REQUIRE(heads_dk(c) <= 128, 3, "attention head size above 128 is not implemented");
+  TTS_REQUIRE(c.kernel_size == 1 || c.kernel_size == 3 || c.kernel_size == 5 || c.kernel_size == 7 ||
+                  c.kernel_size == 11,
+              3, "FFN kernel_size must be 1, 3, 5, 7 or 11");
+  TTS_REQUIRE(c.rel_attn_window_size >= 0, 1, "rel_attn_window_size must be >= 0 (0 = None)");
+  TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned duration predictor (c_in_channels > 0) not implemented");
+  TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
+  TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3,
+              "Glow encoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
+}
+
+GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, int device)
+    : cfg_(cfg), device_(device) {
+  glow_encoder_validate(cfg_);
+  DeviceGuard g(device_);
+  const auto shapes = glow_encoder_weight_shapes(cfg_);
+  for (size_t i = 0; i < shapes.size(); ++i)
+    TTS_REQUIRE(hw[i] != nullptr, 1, "weight pointer " + std::to_string(i) + " is NULL");
+  const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, K = cfg_.kernel_size;
+  const int D = cfg_.hidden_channels_dp;
+  const int mode = cfg_.math_mode;
+
+  std::vector<float> host;
+  std::vector<std::pair<size_t, float**>> fix;
+  auto align = [](size_t n) { return (n + 63) & ~size_t(63); };
+  auto put = [&](const float* src, size_t n, float** dst) {
+    const size_t off = host.size();
+    host.resize(off + align(n), 0.f);
+    std::memcpy(host.data() + off, src, n * sizeof(float));
+    fix.push_back({off, dst});
+  };
+  // conv from one or more row blocks of torch weights [rows][Cin][K] stacked along Cout
+  auto put_conv = [&](Conv& cv, std::vector<std::pair<const float*, const float*>> parts, int rows_each, int Cin,
+                      int k) {
+    const int Cout = rows_each * (int)parts.size();
+    cv.Cin = Cin; cv.Cout = Cout; cv.K = k;
+    cv.tile = conv_tile_for(mode, Cout, k, Cin, 1, false);
+    const ConvTile t = conv_tile(mode, cv.tile);
+    cv.n_chunks = ceil_div(Cin, t.CK);
+    std::vector<float> w((size_t)Cout * Cin * k), b(Cout);
+    for (size_t p = 0; p < parts.size(); ++p) {
+      std::memcpy(w.data() + p * (size_t)rows_each * Cin * k, parts[p].first, sizeof(float) * rows_each * Cin * k);
+      std::memcpy(b.data() + p * rows_each, parts[p].second, sizeof(float) * rows_each);
+    }
+    const size_t n = packed_conv_numel(mode, Cout, Cin, k, t);
+    const size_t off = host.size();
+    host.resize(off + align(n), 0.f);
+    const int w_exp = pack_conv(mode, w.data(), Cout, Cin, k, t, host.data() + off);
+    TTS_REQUIRE(w_exp == 0, 3, "Glow encoder: scaled weight packing is not supported");
+    fix.push_back({off, &cv.w});
+    const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
+    const size_t offb = host.size();
+    host.resize(offb + align(nb), 0.f);
+    std::memcpy(host.data() + offb, b.data(), Cout * sizeof(float));
+    fix.push_back({offb, &cv.b});
+  };
+  auto put_norm = [&](Norm& n, const float* gm, const float* bt, int C) {
+    put(gm, C, &n.gamma);
+    put(bt, C, &n.beta);
+  };
+
+  size_t wi = 0;
+  put(hw[wi++], (size_t)cfg_.num_chars * H, &emb_);
+  if (cfg_.use_prenet) {
+    for (int l = 0; l < 3; ++l) {
+      put_conv(pre_conv_[l], {{hw[wi], hw[wi + 1]}}, H, H, 5);
+      put_norm(pre_norm_[l], hw[wi + 2], hw[wi + 3], H);
+      wi += 4;
+    }
+    put_conv(pre_proj_, {{hw[wi], hw[wi + 1]}}, H, H, 1);
+    wi += 2;
+  }
+  layers_.resize(cfg_.num_layers);
+  for (int l = 0; l < cfg_.num_layers; ++l) {
+    Layer& L = layers_[l];
+    put_conv(L.qkv, {{hw[wi], hw[wi + 1]}, {hw[wi + 2], hw[wi + 3]}, {hw[wi + 4], hw[wi + 5]}}, H, H, 1);
+    put_conv(L.o, {{hw[wi + 6], hw[wi + 7]}}, H, H, 1);
+    wi += 8;
+    if (cfg_.rel_attn_window_size > 0) {
+      const size_t R = 2 * cfg_.rel_attn_window_size + 1;
+      put(hw[wi], R * heads_dk(cfg_), &L.ek);
+      put(hw[wi + 1], R * heads_dk(cfg_), &L.ev);
+      wi += 2;
+    }
+    put_norm(L.n1, hw[wi], hw[wi + 1], H);
+    put_conv(L.ffn1, {{hw[wi + 2], hw[wi + 3]}}, F, H, K);
+    put_conv(L.ffn2, {{hw[wi + 4], hw[wi + 5]}}, H, F, K);
+    put_norm(L.n2, hw[wi + 6], hw[wi + 7], H);
+    wi += 8;
+  }
+  put_conv(proj_m_, {{hw[wi], hw[wi + 1]}}, cfg_.out_channels, H, 1);
+  wi += 2;
+  if (!cfg_.mean_only) {
+    put_conv(proj_s_, {{hw[wi], hw[wi + 1]}}, cfg_.out_channels, H, 1);
+    wi += 2;
+  }
+  put_conv(dp1_, {{hw[wi], hw[wi + 1]}}, D, H, 3);
+  put_norm(dpn1_, hw[wi + 2], hw[wi + 3], D);
+  put_conv(dp2_, {{hw[wi + 4], hw[wi + 5]}}, D, D, 3);
+  put_norm(dpn2_, hw[wi + 6], hw[wi + 7], D);
+  put_conv(dp_proj_, {{hw[wi + 8], hw[wi + 9]}}, 1, D, 1);
+  wi += 10;
+  TTS_REQUIRE(wi == shapes.size(), 2, "internal: Glow encoder weight count mismatch");
+
+  if (hipMalloc(&arena_, host.size() * sizeof(float)) != hipSuccess) throw Error(4, "hipMalloc(weights) failed");
+  TTS_HIP_CHECK(hipMemcpy(arena_, host.data(), host.size() * sizeof(float), hipMemcpyHostToDevice));
+  for (auto& p : fix) *p.second = arena_ + p.first;
+}
+
+GlowEncoder::~GlowEncoder() {
+  DeviceGuard g(device_);
+  if (arena_) (void)hipFree(arena_);
+  if (ws_) (void)hipFree(ws_);
+}
+
+void GlowEncoder::reserve(int B, int T) {
+  const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, D = cfg_.hidden_channels_dp;
+  const size_t plane = (size_t)B * T;
+  const size_t big = std::max({(size_t)3 * H, (size_t)F, (size_t)D});
+  const size_t need = plane * (3 * (size_t)H + big + std::max((size_t)H, (size_t)D)) * sizeof(float) + 4096;
+  if (need <= ws_bytes_) return;
+  if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
+  if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
+  ws_bytes_ = need;
+}
+
+void GlowEncoder::forward(const int64_t* tok, const int64_t* len, int B, int T, float* x_m, float* x_logs,
+                          float* logw, float* x_mask, hipStream_t s, Profiler* prof) {
+  TTS_REQUIRE(tok && len && x_m && logw && x_mask, 1, "NULL input/output pointer");
+  TTS_REQUIRE(B >= 1 && T >= 1, 1, "batch and token count must be >= 1");
+  TTS_REQUIRE(T <= ATTN_MAX_T, 3, "more than " + std::to_string(ATTN_MAX_T) + " tokens per utterance");
+  DeviceGuard g(device_);
+  reserve(B, T);
+  const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, D = cfg_.hidden_channels_dp;
+  const int mode = cfg_.math_mode;
+  const size_t plane = (size_t)B * T;
+  const double P = (double)plane;
+  auto al = [](size_t n) { return (n + 63) & ~size_t(63); };
+  float* p = ws_;
+  float* X0 = p; p += al(plane * H);   // layer state ping
+  float* X1 = p; p += al(plane * H);   // layer state pong
+  float* A = p; p += al(plane * H);    // attention output
+  const size_t big = std::max({(size_t)3 * H, (size_t)F, (size_t)D});
+  float* Wd = p; p += al(plane * big);  // qkv / FFN hidden / dp hidden
+  float* Nb = p;                         // LayerNorm output of prenet / dp (max(H, D) rows)
+  const float* mask = x_mask;
+  constexpr float kEps = 1e-4f;  // normalization.py:6
+
+  auto conv = [&](const char* name, const Conv& cv, const float* in, float* out, const float* res, const float* m,
+                  float out_slope, bool mask_res) {
+    Conv1dArgs a{};
+    a.x = in; a.w = cv.w; a.bias = cv.b; a.y = out; a.res = res; a.mask = m;
+    a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = T; a.Tout = T;
+    a.dil = 1; a.pad = (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;  // same padding (transformer.py:335)
+    a.in_slope = 1.f; a.out_slope = out_slope; a.zmode = 0; a.zdiv = 1.f;
+    a.mask_res = mask_res ? 1 : 0;
+    run(prof, s, name, 2.0 * P * cv.Cout * cv.Cin * cv.K, 4.0 * P * (cv.Cin + cv.Cout + (res ? cv.Cout : 0)),
+        [&] { launch_conv(mode, a, B, cv.K, cv.tile, s); });
+  };
+  auto norm = [&](const char* name, const Norm& n, const float* a, const float* r, float* y, int C, bool relu) {
+    run(prof, s, name, 0.0, 4.0 * P * C * (r ? 3 : 2),
+        [&] { launch_layernorm(a, r, n.gamma, n.beta, mask, y, B, C, T, kEps, relu, s); });
+  };
+
+  // emb(x) * sqrt(H), transpose, x_mask (encoder.py:162-164)
+  const float scale = (float)std::sqrt((double)H);
+  run(prof, s, "enc_embed", 0.0, 4.0 * P * H + 16.0 * P,
+      [&] { launch_embed(tok, len, emb_, X0, x_mask, B, H, T, cfg_.num_chars, scale, s); });
+  float* x = X0;
+  if (cfg_.use_prenet) {  // glow.py:61-67
+    const float* in = X0;
+    for (int l = 0; l < 3; ++l) {
+      conv("enc_prenet_conv", pre_conv_[l], in, Wd, nullptr, mask, 1.f, false);
+      norm("enc_layernorm", pre_norm_[l], Wd, nullptr, Nb, H, true);  // LN(x*mask) -> relu
+      in = Nb;
+    }
+    conv("enc_prenet_proj", pre_proj_, Nb, X1, X0, mask, 1.f, true);  // (x_res + proj(x)) * mask
+    x = X1;
+  }
+  // transformer layers (transformer.py:420-431); x is masked on entry
+  for (int l = 0; l < cfg_.num_layers; ++l) {
+    const Layer& L = layers_[l];
+    float* other = (x == X0) ? X1 : X0;
+    conv("enc_qkv", L.qkv, x, Wd, nullptr, nullptr, 1.f, false);
+    run(prof, s, "enc_attention", 4.0 * (double)B * T * T * H, 4.0 * P * 4 * H, [&] {
+      launch_attention(Wd, mask, L.ek, L.ev, A, B, H, cfg_.num_heads, T, cfg_.rel_attn_window_size, s);
+    });
+    conv("enc_attn_o", L.o, A, other, x, nullptr, 1.f, false);          // x + conv_o(attn)
+    norm("enc_layernorm", L.n1, other, nullptr, other, H, false);         // norm_layers_1, * mask
+    conv("enc_ffn1", L.ffn1, other, Wd, nullptr, mask, 0.f, false);      // relu(conv_1(x*mask)) * mask
+    conv("enc_ffn2", L.ffn2, Wd, x, other, mask, 1.f, false);            // x + conv_2(h*mask)*mask
+    norm("enc_layernorm", L.n2, x, nullptr, x, H, false);                 // norm_layers_2, * mask
+  }
+  // heads (encoder.py:171-178)
+  conv("enc_proj_m", proj_m_, x, x_m, nullptr, mask, 1.f, false);
+  if (!cfg_.mean_only) {
+    TTS_REQUIRE(x_logs != nullptr, 1, "x_logs is NULL (mean_only = 0)");
+    conv("enc_proj_s", proj_s_, x, x_logs, nullptr, mask, 1.f, false);
+  } else if (x_logs) {
+    TTS_HIP_CHECK(hipMemsetAsync(x_logs, 0, plane * cfg_.out_channels * sizeof(float), s));
+  }
+  // duration predictor (duration_predictor.py:63-73) on x (detached: same values)
+  conv("enc_dp_conv", dp1_, x, Wd, nullptr, mask, 0.f, false);
+  norm("enc_layernorm", dpn1_, Wd, nullptr, Nb, D, false);
+  conv("enc_dp_conv", dp2_, Nb, Wd, nullptr, mask, 0.f, false);
+  norm("enc_layernorm", dpn2_, Wd, nullptr, Nb, D, false);
+  conv("enc_dp_proj", dp_proj_, Nb, logw, nullptr, mask, 1.f, false);
+  (void)F;
+}
+
+}  // namespace tts

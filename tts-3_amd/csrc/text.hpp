@@ -1,0 +1,90 @@
+// Glow-TTS text side: encoder executor (glow_encoder.cpp) and its kernels (kernels_text.hip).
+// Reference: TTS/tts/layers/glow_tts/encoder.py:83-179, transformer.py, duration_predictor.py,
+// glow.py:11-67 (prenet), TTS/tts/models/glow_tts.py:342-363 (inference glue).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "hifigan.hpp"
+#include "tts_mi355x.h"
+
+namespace tts {
+
+constexpr int ATTN_MAX_T = 3072;     // tokens per utterance (score rows live in LDS)
+constexpr int EXPAND_MAX_TX = 16384;  // tokens per utterance of the alignment expansion (LDS cumsum)
+
+void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, float* x, float* mask, int B, int H,
+                  int T, int num_chars, float scale, hipStream_t s);
+// y = LN_C(a [+ r]) * gamma + beta [relu] * mask (mask may be NULL); y may alias a or r
+void launch_layernorm(const float* a, const float* r, const float* gamma, const float* beta, const float* mask,
+                      float* y, int B, int C, int T, float eps, bool relu, hipStream_t s);
+// out[B][H][T] = multi-head attention of qkv [B][3H][T] (W = 0: no relative embeddings)
+void launch_attention(const float* qkv, const float* mask, const float* ek, const float* ev, float* out, int B,
+                      int H, int heads, int T, int W, hipStream_t s);
+void launch_durations(const float* logw, const float* xm, float* w_ceil, int64_t* y_len, float* dur, int B, int T,
+                      float length_scale, hipStream_t s);
+
+struct ExpandArgs {
+  const float* w_ceil;       // [B][T_x]
+  const float* x_mask;       // [B][T_x]
+  const int64_t* y_len;      // [B]
+  const float* o_mean;       // [B][C][T_x]
+  const float* o_log_scale;  // [B][C][T_x] or NULL (zeros: mean_only)
+  const float* noise;        // [B][C][T_y] or NULL (zeros)
+  float noise_scale;
+  int C, T_x, T_y;
+  float* z;                  // [B][C][T_y]
+  float* y_mask;             // [B][T_y]
+  float* y_mean;             // [B][C][T_y] or NULL
+  float* y_log_scale;        // [B][C][T_y] or NULL
+  float* attn;               // [B][T_x][T_y] or NULL
+};
+void launch_expand(const ExpandArgs& a, int B, hipStream_t s);
+
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c);
+void glow_encoder_validate(const TtsGlowEncoderCfg& c);
+
+class GlowEncoder {
+ public:
+  GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* host_weights, int device);
+  ~GlowEncoder();
+  GlowEncoder(const GlowEncoder&) = delete;
+  GlowEncoder& operator=(const GlowEncoder&) = delete;
+  void forward(const int64_t* tok, const int64_t* len, int B, int T, float* x_m, float* x_logs, float* logw,
+               float* x_mask, hipStream_t s, Profiler* prof = nullptr);
+  int device() const { return device_; }
+
+ private:
+  struct Conv {
+    int Cin = 0, Cout = 0, K = 1, tile = 0, n_chunks = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+  };
+  struct Norm {
+    float* gamma = nullptr;
+    float* beta = nullptr;
+  };
+  struct Layer {
+    Conv qkv, o, ffn1, ffn2;
+    float* ek = nullptr;
+    float* ev = nullptr;
+    Norm n1, n2;
+  };
+  void reserve(int B, int T);
+
+  TtsGlowEncoderCfg cfg_;
+  int device_;
+  float* emb_ = nullptr;
+  Conv pre_conv_[3], pre_proj_;
+  Norm pre_norm_[3];
+  std::vector<Layer> layers_;
+  Conv proj_m_, proj_s_, dp1_, dp2_, dp_proj_;
+  Norm dpn1_, dpn2_;
+  float* arena_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+}  // namespace tts

@@ -69,6 +69,24 @@ class TtsGlowDecoderCfg(Structure):
     ]
 
 
+class TtsGlowEncoderCfg(Structure):
+    _fields_ = [
+        ("num_chars", c_int),
+        ("out_channels", c_int),
+        ("hidden_channels", c_int),
+        ("hidden_channels_dp", c_int),
+        ("hidden_channels_ffn", c_int),
+        ("num_heads", c_int),
+        ("num_layers", c_int),
+        ("kernel_size", c_int),
+        ("rel_attn_window_size", c_int),
+        ("mean_only", c_int),
+        ("use_prenet", c_int),
+        ("c_in_channels", c_int),
+        ("math_mode", c_int),
+    ]
+
+
 class TtsVitsFlowCfg(Structure):
     _fields_ = [
         ("channels", c_int),
@@ -137,6 +155,28 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_glow_encoder_num_weights": (c_int, [POINTER(TtsGlowEncoderCfg)]),
+    "tts_glow_encoder_weight_numel": (c_int64, [POINTER(TtsGlowEncoderCfg), c_int]),
+    "tts_glow_encoder_create": (
+        c_int, [POINTER(TtsGlowEncoderCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]
+    ),
+    "tts_glow_encoder_destroy": (c_int, [c_void_p]),
+    "tts_glow_encoder_forward": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    ),
+    "tts_glow_encoder_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_glow_durations": (
+        c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]
+    ),
+    "tts_glow_expand": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int, c_int,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "tts_vits_flow_num_weights": (c_int, [POINTER(TtsVitsFlowCfg)]),
     "tts_vits_flow_weight_numel": (c_int64, [POINTER(TtsVitsFlowCfg), c_int]),

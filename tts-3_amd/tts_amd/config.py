@@ -3,6 +3,8 @@ JSON reader (no coqpit dependency).
 
 * ``HIFIGAN_V1``: ``HifiganConfig.generator_model_params`` (TTS/vocoder/configs/hifigan_config.py:95-104)
 * ``GLOW_TTS_DECODER``: the decoder fields of ``GlowTTSConfig`` (TTS/tts/configs/glow_tts_config.py:117-131)
+* ``GLOW_TTS_ENCODER``: the encoder fields of ``GlowTTSConfig`` (glow_tts_config.py:103-124) as
+  ``GlowTTS.__init__`` hands them to ``Encoder`` (TTS/tts/models/glow_tts.py:80-91)
 * ``VITS_FLOW`` / ``VITS_DECODER``: the flow and waveform-decoder fields of ``VitsArgs``
   (TTS/tts/models/vits.py:545-565, built at :675-682 and :704-718)
 """
@@ -33,6 +35,23 @@ GLOW_TTS_DECODER: Dict[str, Any] = {
     "sigmoid_scale": False,
     "c_in_channels": 0,
 }
+
+GLOW_TTS_ENCODER: Dict[str, Any] = {
+    "out_channels": 80,
+    "hidden_channels": 192,     # hidden_channels_enc
+    "hidden_channels_dp": 256,
+    "encoder_type": "rel_pos_transformer",
+    "encoder_params": {"kernel_size": 3, "dropout_p": 0.1, "num_layers": 6, "num_heads": 2,
+                       "hidden_channels_ffn": 768},
+    "dropout_p_dp": 0.1,
+    "mean_only": True,
+    "use_prenet": True,         # use_encoder_prenet
+    "c_in_channels": 0,
+}
+
+# GlowTTS.inference glue (glow_tts.py:342-363): GlowTTSConfig defaults.  The dataclass declares
+# inference_noise_scale twice (glow_tts_config.py:124 = 0.33, :151 = 0.0); the later one wins.
+GLOW_TTS_INFERENCE: Dict[str, Any] = {"length_scale": 1.0, "inference_noise_scale": 0.0}
 
 VITS_FLOW: Dict[str, Any] = {
     "channels": 192,            # hidden_channels

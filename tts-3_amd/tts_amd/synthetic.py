@@ -23,7 +23,7 @@ from typing import Dict, List, Sequence
 import numpy as np
 import torch
 
-from .config import HIFIGAN_V1, GLOW_TTS_DECODER, VITS_FLOW
+from .config import HIFIGAN_V1, GLOW_TTS_DECODER, GLOW_TTS_ENCODER, VITS_FLOW
 
 
 def _wn_pair(rng, v: np.ndarray):
@@ -211,6 +211,89 @@ def vits_flow_state_dict(
             wn_conv(f"{pre}.enc.cond_layer", 2 * H * num_layers, cond_channels, 1, 0.5)
         conv(f"{pre}.post", half, H, 1, 0.3)
     return sd
+
+
+def glow_encoder_state_dict(
+    num_chars: int = 64,
+    out_channels: int = GLOW_TTS_ENCODER["out_channels"],
+    hidden_channels: int = GLOW_TTS_ENCODER["hidden_channels"],
+    hidden_channels_dp: int = GLOW_TTS_ENCODER["hidden_channels_dp"],
+    encoder_params: Dict = None,
+    mean_only: bool = GLOW_TTS_ENCODER["mean_only"],
+    use_prenet: bool = GLOW_TTS_ENCODER["use_prenet"],
+    seed: int = 8642,
+    log_duration: float = 1.6,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a Glow-TTS ``Encoder`` (TTS/tts/layers/glow_tts/encoder.py:83-152,
+    rel_pos_transformer) with synthetic weights, in the reference's key order.
+
+    * embedding ~ N(0, H^-0.5) as the reference (:102), so emb * sqrt(H) has unit variance
+    * convs variance-preserving (1x1 q/k/v/o, FFN k3, duration predictor k3); the prenet's
+      zero-initialised ``proj`` (glow.py:51-53) is randomised, otherwise the prenet is identity
+    * LayerNorm gamma ~ 1 + 0.1 N, beta ~ 0.1 N (reference init 0.1 / 0: a weak test)
+    * duration ``proj`` bias = ``log_duration`` with small weights, so exp(logw) - 1 is a few
+      frames per token (a random-init predictor clamps every duration to 1)
+    """
+    ep = dict(GLOW_TTS_ENCODER["encoder_params"]) if encoder_params is None else dict(encoder_params)
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    H = hidden_channels
+    F_ = ep["hidden_channels_ffn"]
+    K = ep.get("kernel_size", 1)
+    nh = ep["num_heads"]
+    W = ep.get("rel_attn_window_size")
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+
+    def conv(name: str, cout: int, cin: int, k: int, scale: float = 1.0, bias_std: float = 0.02):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        sd[f"{name}.weight"] = t(w)
+        sd[f"{name}.bias"] = t(rng.standard_normal((cout,)) * bias_std)
+
+    def norm(name: str, c: int):
+        sd[f"{name}.gamma"] = t(1.0 + 0.1 * rng.standard_normal((1, c, 1)))
+        sd[f"{name}.beta"] = t(0.1 * rng.standard_normal((1, c, 1)))
+
+    sd["emb.weight"] = t(rng.standard_normal((num_chars, H)) * H**-0.5)
+    if use_prenet:
+        for l in range(3):
+            conv(f"prenet.conv_layers.{l}", H, H, 5)
+        for l in range(3):
+            norm(f"prenet.norm_layers.{l}", H)
+        conv("prenet.proj", H, H, 1, 0.5)
+    for l in range(ep["num_layers"]):
+        pre = f"encoder.attn_layers.{l}"
+        for n in ("q", "k", "v", "o"):
+            conv(f"{pre}.conv_{n}", H, H, 1)
+        if W is not None:
+            kc = H // nh
+            sd[f"{pre}.emb_rel_k"] = t(rng.standard_normal((1, 2 * W + 1, kc)) * kc**-0.5)
+            sd[f"{pre}.emb_rel_v"] = t(rng.standard_normal((1, 2 * W + 1, kc)) * kc**-0.5)
+    for l in range(ep["num_layers"]):
+        norm(f"encoder.norm_layers_1.{l}", H)
+    for l in range(ep["num_layers"]):
+        conv(f"encoder.ffn_layers.{l}.conv_1", F_, H, K, 1.4)  # relu halves the variance
+        conv(f"encoder.ffn_layers.{l}.conv_2", H, F_, K)
+    for l in range(ep["num_layers"]):
+        norm(f"encoder.norm_layers_2.{l}", H)
+    conv("proj_m", out_channels, H, 1)
+    if not mean_only:
+        conv("proj_s", out_channels, H, 1, 0.3)
+    conv("duration_predictor.conv_1", hidden_channels_dp, H, 3, 1.4)
+    norm("duration_predictor.norm_1", hidden_channels_dp)
+    conv("duration_predictor.conv_2", hidden_channels_dp, hidden_channels_dp, 3, 1.4)
+    norm("duration_predictor.norm_2", hidden_channels_dp)
+    conv("duration_predictor.proj", 1, hidden_channels_dp, 1, 0.3)
+    sd["duration_predictor.proj.bias"] = t(np.full((1,), log_duration))
+    return sd
+
+
+def tokens(batch: int, length: int, num_chars: int, seed: int = 0) -> torch.Tensor:
+    """Synthetic token ids [B, T] uniform in [0, num_chars) (int64, CPU)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, num_chars, (batch, length), generator=g)
 
 
 def mel(batch: int, frames: int, channels: int = 80, seed: int = 0) -> torch.Tensor:

@@ -1,6 +1,7 @@
-"""Acoustic-model surface: the Glow-TTS ``Decoder`` and the VITS ``ResidualCouplingBlocks`` flow
-(reverse flows on MI355X)."""
+"""Acoustic-model surface: the Glow-TTS ``Encoder`` / ``Decoder`` / ``GlowTTS.inference`` and the
+VITS ``ResidualCouplingBlocks`` flow, on MI355X."""
 from .glow_decoder import Decoder
+from .glow_tts import Encoder, GlowTTS
 from .vits_flow import ResidualCouplingBlocks
 
-__all__ = ["Decoder", "ResidualCouplingBlocks"]
+__all__ = ["Decoder", "Encoder", "GlowTTS", "ResidualCouplingBlocks"]

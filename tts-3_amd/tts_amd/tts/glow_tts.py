@@ -1,0 +1,425 @@
+"""Drop-in Glow-TTS text side whose inference runs in ``libtts_mi355x.so``.
+
+* ``Encoder`` mirrors ``TTS/tts/layers/glow_tts/encoder.py`` (Coqui TTS 0.22.0) for
+  ``encoder_type="rel_pos_transformer"``: same constructor (:83-95), same parameter tree
+  (``emb``, ``prenet.{conv_layers,norm_layers,proj}``, ``encoder.{attn_layers,norm_layers_1,
+  ffn_layers,norm_layers_2}``, ``proj_m``, ``proj_s``, ``duration_predictor.*``) so reference
+  checkpoints load unchanged; ``forward(x, x_lengths, g=None)`` returns
+  ``(x_m, x_logs, logw, x_mask)`` like :143-179.
+* ``GlowTTS`` is the inference surface of ``TTS/tts/models/glow_tts.py``: ``inference(x,
+  aux_input)`` (:342-374) runs encoder -> durations -> alignment expansion -> decoder reverse
+  on the device and returns the reference's output dict.  ``load_checkpoint`` (:522-530) reads
+  the ``model`` state dict with ``torch.load(weights_only=True)``.
+
+The nn modules below only hold parameters; the handle is rebuilt when any parameter changes.
+The other encoder types (gated_conv, residual_conv_bn, time_depth_separable), speaker
+conditioning and training (``forward``, MAS) are outside the MI355X path and raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from types import SimpleNamespace
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+from torch import nn
+
+from .. import _native as N
+from ..config import GLOW_TTS_DECODER, GLOW_TTS_ENCODER, GLOW_TTS_INFERENCE
+from .glow_decoder import Decoder
+
+
+class LayerNorm(nn.Module):
+    """normalization.py:5-28 (parameters only)."""
+
+    def __init__(self, channels: int, eps: float = 1e-4):
+        super().__init__()
+        self.channels = channels
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(1, channels, 1) * 0.1)
+        self.beta = nn.Parameter(torch.zeros(1, channels, 1))
+
+
+class ResidualConv1dLayerNormBlock(nn.Module):
+    """glow.py:11-67 (parameters only)."""
+
+    def __init__(self, in_channels, hidden_channels, out_channels, kernel_size, num_layers, dropout_p):
+        super().__init__()
+        assert num_layers > 1 and kernel_size % 2 == 1
+        self.kernel_size = kernel_size
+        self.num_layers = num_layers
+        self.conv_layers = nn.ModuleList(
+            [nn.Conv1d(in_channels if i == 0 else hidden_channels, hidden_channels, kernel_size,
+                       padding=kernel_size // 2) for i in range(num_layers)])
+        self.norm_layers = nn.ModuleList([LayerNorm(hidden_channels) for _ in range(num_layers)])
+        self.proj = nn.Conv1d(hidden_channels, out_channels, 1)
+
+
+class RelativePositionMultiHeadAttention(nn.Module):
+    """transformer.py:10-115 (parameters only)."""
+
+    def __init__(self, channels, out_channels, num_heads, rel_attn_window_size=None, heads_share=True,
+                 dropout_p=0.0, input_length=None, proximal_bias=False, proximal_init=False):
+        super().__init__()
+        assert channels % num_heads == 0, " [!] channels should be divisible by num_heads."
+        self.num_heads = num_heads
+        self.rel_attn_window_size = rel_attn_window_size
+        self.k_channels = channels // num_heads
+        self.conv_q = nn.Conv1d(channels, channels, 1)
+        self.conv_k = nn.Conv1d(channels, channels, 1)
+        self.conv_v = nn.Conv1d(channels, channels, 1)
+        self.conv_o = nn.Conv1d(channels, out_channels, 1)
+        if rel_attn_window_size is not None:
+            n_heads_rel = 1 if heads_share else num_heads
+            std = self.k_channels**-0.5
+            self.emb_rel_k = nn.Parameter(torch.randn(n_heads_rel, rel_attn_window_size * 2 + 1, self.k_channels) * std)
+            self.emb_rel_v = nn.Parameter(torch.randn(n_heads_rel, rel_attn_window_size * 2 + 1, self.k_channels) * std)
+
+
+class FeedForwardNetwork(nn.Module):
+    """transformer.py:285-341 (parameters only)."""
+
+    def __init__(self, in_channels, out_channels, hidden_channels, kernel_size, dropout_p=0.0, causal=False):
+        super().__init__()
+        self.conv_1 = nn.Conv1d(in_channels, hidden_channels, kernel_size)
+        self.conv_2 = nn.Conv1d(hidden_channels, out_channels, kernel_size)
+
+
+class RelativePositionTransformer(nn.Module):
+    """transformer.py:344-432 (parameters only; in = out = hidden as Encoder builds it)."""
+
+    def __init__(self, in_channels, out_channels, hidden_channels, hidden_channels_ffn, num_heads, num_layers,
+                 kernel_size=1, dropout_p=0.0, rel_attn_window_size=None, input_length=None, layer_norm_type="1"):
+        super().__init__()
+        if layer_norm_type != "1":
+            raise NotImplementedError("layer_norm_type '2' (LayerNorm2) is not implemented on the MI355X path")
+        if input_length is not None:
+            raise NotImplementedError("input_length (block-limited attention) is not implemented on the MI355X path")
+        self.num_layers = num_layers
+        self.attn_layers = nn.ModuleList()
+        self.norm_layers_1 = nn.ModuleList()
+        self.ffn_layers = nn.ModuleList()
+        self.norm_layers_2 = nn.ModuleList()
+        for idx in range(num_layers):
+            self.attn_layers.append(RelativePositionMultiHeadAttention(
+                hidden_channels if idx != 0 else in_channels, hidden_channels, num_heads,
+                rel_attn_window_size=rel_attn_window_size, dropout_p=dropout_p))
+            self.norm_layers_1.append(LayerNorm(hidden_channels))
+            last = (idx + 1) == num_layers
+            self.ffn_layers.append(FeedForwardNetwork(hidden_channels, out_channels if last else hidden_channels,
+                                                      hidden_channels_ffn, kernel_size, dropout_p=dropout_p))
+            self.norm_layers_2.append(LayerNorm(out_channels if last else hidden_channels))
+
+
+class DurationPredictor(nn.Module):
+    """duration_predictor.py:7-73 (parameters only)."""
+
+    def __init__(self, in_channels, hidden_channels, kernel_size, dropout_p, cond_channels=None, language_emb_dim=None):
+        super().__init__()
+        self.conv_1 = nn.Conv1d(in_channels, hidden_channels, kernel_size, padding=kernel_size // 2)
+        self.norm_1 = LayerNorm(hidden_channels)
+        self.conv_2 = nn.Conv1d(hidden_channels, hidden_channels, kernel_size, padding=kernel_size // 2)
+        self.norm_2 = LayerNorm(hidden_channels)
+        self.proj = nn.Conv1d(hidden_channels, 1, 1)
+
+
+def _f32(t: torch.Tensor) -> np.ndarray:
+    return np.ascontiguousarray(t.detach().to("cpu", torch.float32).numpy())
+
+
+class Encoder(nn.Module):
+    def __init__(self, num_chars, out_channels, hidden_channels, hidden_channels_dp, encoder_type, encoder_params,
+                 dropout_p_dp=0.1, mean_only=False, use_prenet=True, c_in_channels=0, math_mode: str = "fp32"):
+        super().__init__()
+        if encoder_type.lower() != "rel_pos_transformer":
+            raise NotImplementedError(f"encoder_type '{encoder_type}' is not implemented on the MI355X path "
+                                      "(only rel_pos_transformer, the Glow-TTS default)")
+        if c_in_channels:
+            raise NotImplementedError("speaker-conditioned duration predictor (c_in_channels > 0) not implemented")
+        if math_mode not in N.MATH_MODES:
+            raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
+        self.num_chars = num_chars
+        self.out_channels = out_channels
+        self.hidden_channels = hidden_channels
+        self.hidden_channels_dp = hidden_channels_dp
+        self.mean_only = mean_only
+        self.use_prenet = use_prenet
+        self.c_in_channels = c_in_channels
+        self.encoder_type = encoder_type
+        self.encoder_params = dict(encoder_params)
+        self.math_mode = math_mode
+        self.emb = nn.Embedding(num_chars, hidden_channels)
+        nn.init.normal_(self.emb.weight, 0.0, hidden_channels**-0.5)
+        if use_prenet:
+            self.prenet = ResidualConv1dLayerNormBlock(hidden_channels, hidden_channels, hidden_channels,
+                                                       kernel_size=5, num_layers=3, dropout_p=0.5)
+        self.encoder = RelativePositionTransformer(hidden_channels, hidden_channels, hidden_channels, **encoder_params)
+        self.proj_m = nn.Conv1d(hidden_channels, out_channels, 1)
+        if not mean_only:
+            self.proj_s = nn.Conv1d(hidden_channels, out_channels, 1)
+        self.duration_predictor = DurationPredictor(hidden_channels + c_in_channels, hidden_channels_dp, 3,
+                                                    dropout_p_dp)
+        ep = self.encoder_params
+        c = N.TtsGlowEncoderCfg()
+        c.num_chars = num_chars
+        c.out_channels = out_channels
+        c.hidden_channels = hidden_channels
+        c.hidden_channels_dp = hidden_channels_dp
+        c.hidden_channels_ffn = ep["hidden_channels_ffn"]
+        c.num_heads = ep["num_heads"]
+        c.num_layers = ep["num_layers"]
+        c.kernel_size = ep.get("kernel_size", 1)
+        c.rel_attn_window_size = ep.get("rel_attn_window_size") or 0
+        c.mean_only = 1 if mean_only else 0
+        c.use_prenet = 1 if use_prenet else 0
+        c.c_in_channels = c_in_channels
+        c.math_mode = N.MATH_MODES[math_mode]
+        self._cfg = c
+        self._handle = None
+        self._handle_key = None
+        n = N.lib().tts_glow_encoder_num_weights(ctypes.byref(c))
+        if n < 0:
+            N.check("tts_glow_encoder_num_weights", -n)
+
+    # ------------------------------------------------------------------ native handle
+    def _weight_list(self) -> List[np.ndarray]:
+        ws: List[np.ndarray] = [_f32(self.emb.weight)]
+
+        def conv(m):
+            ws.extend([_f32(m.weight), _f32(m.bias)])
+
+        def norm(m):
+            ws.extend([_f32(m.gamma).reshape(-1), _f32(m.beta).reshape(-1)])
+
+        if self.use_prenet:
+            for l in range(3):
+                conv(self.prenet.conv_layers[l])
+                norm(self.prenet.norm_layers[l])
+            conv(self.prenet.proj)
+        enc = self.encoder
+        for l in range(enc.num_layers):
+            a = enc.attn_layers[l]
+            for m in (a.conv_q, a.conv_k, a.conv_v, a.conv_o):
+                conv(m)
+            if a.rel_attn_window_size is not None:
+                if a.emb_rel_k.size(0) != 1:
+                    raise NotImplementedError("heads_share=False relative embeddings are not implemented")
+                ws.extend([_f32(a.emb_rel_k), _f32(a.emb_rel_v)])
+            norm(enc.norm_layers_1[l])
+            conv(enc.ffn_layers[l].conv_1)
+            conv(enc.ffn_layers[l].conv_2)
+            norm(enc.norm_layers_2[l])
+        conv(self.proj_m)
+        if not self.mean_only:
+            conv(self.proj_s)
+        dp = self.duration_predictor
+        conv(dp.conv_1)
+        norm(dp.norm_1)
+        conv(dp.conv_2)
+        norm(dp.norm_2)
+        conv(dp.proj)
+        return [np.ascontiguousarray(w) for w in ws]
+
+    def _device(self) -> torch.device:
+        dev = next(self.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("Encoder (tts_amd) runs only on a ROCm device: move it with .to('cuda') first")
+        return dev
+
+    def _native_handle(self):
+        key = tuple((p.data_ptr(), p._version, p.device) for p in self.parameters())
+        if self._handle is not None and key == self._handle_key:
+            return self._handle
+        self._release()
+        dev = self._device()
+        ws = self._weight_list()
+        lib = N.lib()
+        for i, w in enumerate(ws):
+            n = lib.tts_glow_encoder_weight_numel(ctypes.byref(self._cfg), i)
+            if n != w.size:
+                raise ValueError(f"weight {i} has {w.size} elements, expected {n}")
+        arr = (ctypes.c_void_p * len(ws))(*[w.ctypes.data for w in ws])
+        h = ctypes.c_void_p()
+        N.call("tts_glow_encoder_create", ctypes.byref(self._cfg), arr, dev.index or 0, ctypes.byref(h))
+        self._handle, self._handle_key = h, key
+        return h
+
+    def _release(self):
+        if getattr(self, "_handle", None) is not None:
+            N.lib().tts_glow_encoder_destroy(self._handle)
+            self._handle = None
+            self._handle_key = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def _apply(self, fn, *args, **kwargs):
+        self._release()
+        return super()._apply(fn, *args, **kwargs)
+
+    def _io(self, x, x_lengths):
+        dev = self._device()
+        tok = x.to(device=dev, dtype=torch.int64).contiguous()
+        lens = x_lengths.to(device=dev, dtype=torch.int64).contiguous()
+        B, T = tok.shape
+        if lens.shape != (B,):
+            raise ValueError(f"x_lengths must be [B] = [{B}], got {tuple(lens.shape)}")
+        x_m = torch.empty(B, self.out_channels, T, device=dev)
+        x_logs = torch.empty_like(x_m)
+        logw = torch.empty(B, 1, T, device=dev)
+        x_mask = torch.empty(B, 1, T, device=dev)
+        return dev, tok, lens, (x_m, x_logs, logw, x_mask)
+
+    # ------------------------------------------------------------------ reference API
+    def forward(self, x: torch.Tensor, x_lengths: torch.Tensor, g: Optional[torch.Tensor] = None):
+        """encoder.py:143-179: x [B, T] token ids, x_lengths [B] -> (x_m, x_logs, logw, x_mask)."""
+        if g is not None:
+            raise NotImplementedError("speaker conditioning (g) is not implemented on the MI355X path")
+        with torch.no_grad():
+            h = self._native_handle()
+            dev, tok, lens, outs = self._io(x, x_lengths)
+            B, T = tok.shape
+            N.call("tts_glow_encoder_forward", h, N.ptr(tok), N.ptr(lens), B, T, *[N.ptr(o) for o in outs],
+                   N.stream_ptr(dev))
+        return outs
+
+    def profile(self, x: torch.Tensor, x_lengths: torch.Tensor):
+        """One forward with a hipEvent pair around every launch: (outputs, [{name, flops, bytes, ms}])."""
+        h = self._native_handle()
+        dev, tok, lens, outs = self._io(x, x_lengths)
+        B, T = tok.shape
+        cap = 1024
+        recs = (N.TtsLaunchRecord * cap)()
+        n = ctypes.c_int(0)
+        N.call("tts_glow_encoder_forward_profiled", h, N.ptr(tok), N.ptr(lens), B, T, *[N.ptr(o) for o in outs],
+               N.stream_ptr(dev), recs, cap, ctypes.byref(n))
+        rows = [{"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
+                for i in range(min(n.value, cap))]
+        return outs, rows
+
+
+def _cfg_get(config, key, default):
+    if config is None:
+        return default
+    if isinstance(config, dict):
+        return config.get(key, default)
+    return getattr(config, key, default)
+
+
+class GlowTTS(nn.Module):
+    """Inference surface of ``TTS/tts/models/glow_tts.py`` (GlowTTS, :22-530) on the MI355X path.
+
+    ``config`` is a ``GlowTTSConfig``-like object or dict with the reference's field names
+    (glow_tts_config.py:103-152); missing fields take the reference defaults.  ``num_chars`` is
+    required (the reference takes it from the tokenizer, glow_tts.py:63-66).
+    ``math_mode`` / ``decoder_math_mode`` select the conv arithmetic (encoder fp32 by default:
+    the durations are ceil()-quantised, so the encoder keeps exact fp32 arithmetic)."""
+
+    def __init__(self, config=None, math_mode: str = "fp32", decoder_math_mode: Optional[str] = None, **overrides):
+        super().__init__()
+        cfg = dict(overrides)
+
+        def get(key, default):
+            return cfg[key] if key in cfg else _cfg_get(config, key, default)
+
+        self.num_chars = get("num_chars", None)
+        if self.num_chars is None:
+            raise ValueError("num_chars is required")
+        self.out_channels = get("out_channels", GLOW_TTS_ENCODER["out_channels"])
+        self.encoder_type = get("encoder_type", GLOW_TTS_ENCODER["encoder_type"])
+        self.encoder_params = dict(get("encoder_params", GLOW_TTS_ENCODER["encoder_params"]))
+        self.encoder_params.pop("dropout_p", None)
+        if self.encoder_params.get("input_length", None) is None:
+            self.encoder_params.pop("input_length", None)
+        self.hidden_channels_enc = get("hidden_channels_enc", GLOW_TTS_ENCODER["hidden_channels"])
+        self.hidden_channels_dec = get("hidden_channels_dec", GLOW_TTS_DECODER["hidden_channels"])
+        self.hidden_channels_dp = get("hidden_channels_dp", GLOW_TTS_ENCODER["hidden_channels_dp"])
+        self.mean_only = get("mean_only", GLOW_TTS_ENCODER["mean_only"])
+        self.use_encoder_prenet = get("use_encoder_prenet", GLOW_TTS_ENCODER["use_prenet"])
+        self.num_flow_blocks_dec = get("num_flow_blocks_dec", GLOW_TTS_DECODER["num_flow_blocks"])
+        self.kernel_size_dec = get("kernel_size_dec", GLOW_TTS_DECODER["kernel_size"])
+        self.dilation_rate = get("dilation_rate", GLOW_TTS_DECODER["dilation_rate"])
+        self.num_block_layers = get("num_block_layers", GLOW_TTS_DECODER["num_coupling_layers"])
+        self.num_splits = get("num_splits", GLOW_TTS_DECODER["num_splits"])
+        self.num_squeeze = get("num_squeeze", GLOW_TTS_DECODER["num_squeeze"])
+        self.sigmoid_scale = get("sigmoid_scale", GLOW_TTS_DECODER["sigmoid_scale"])
+        self.c_in_channels = get("c_in_channels", 0)
+        self.inference_noise_scale = get("inference_noise_scale", GLOW_TTS_INFERENCE["inference_noise_scale"])
+        self.length_scale = get("length_scale", GLOW_TTS_INFERENCE["length_scale"])
+        if get("use_speaker_embedding", False) or get("use_d_vector_file", False) or self.c_in_channels:
+            raise NotImplementedError("multi-speaker Glow-TTS is not implemented on the MI355X path")
+        self.encoder = Encoder(self.num_chars, out_channels=self.out_channels,
+                               hidden_channels=self.hidden_channels_enc, hidden_channels_dp=self.hidden_channels_dp,
+                               encoder_type=self.encoder_type, encoder_params=self.encoder_params,
+                               mean_only=self.mean_only, use_prenet=self.use_encoder_prenet,
+                               dropout_p_dp=get("dropout_p_dp", 0.1), c_in_channels=0, math_mode=math_mode)
+        self.decoder = Decoder(self.out_channels, self.hidden_channels_dec, self.kernel_size_dec, self.dilation_rate,
+                               self.num_flow_blocks_dec, self.num_block_layers,
+                               dropout_p=get("dropout_p_dec", 0.05), num_splits=self.num_splits,
+                               num_squeeze=self.num_squeeze, sigmoid_scale=self.sigmoid_scale, c_in_channels=0,
+                               math_mode=decoder_math_mode or math_mode)
+
+    def _device(self) -> torch.device:
+        return self.encoder._device()
+
+    @torch.no_grad()
+    def inference(self, x, aux_input={"x_lengths": None, "d_vectors": None, "speaker_ids": None}):  # noqa: B006
+        """glow_tts.py:342-374.  ``aux_input["noise"]`` (optional, [B, out, T_y]) replaces
+        ``torch.randn_like(y_mean)`` so that a caller can pin the sampling noise."""
+        if aux_input.get("d_vectors") is not None or aux_input.get("speaker_ids") is not None:
+            raise NotImplementedError("multi-speaker Glow-TTS is not implemented on the MI355X path")
+        x_lengths = aux_input["x_lengths"]
+        dev = self._device()
+        o_mean, o_log_scale, o_dur_log, x_mask = self.encoder(x, x_lengths)
+        B, C, T_x = o_mean.shape
+        w_ceil = torch.empty(B, 1, T_x, device=dev)
+        y_lengths = torch.empty(B, dtype=torch.int64, device=dev)
+        o_attn_dur = torch.empty(B, 1, T_x, device=dev)
+        stream = N.stream_ptr(dev)
+        N.call("tts_glow_durations", N.ptr(o_dur_log), N.ptr(x_mask), B, T_x, float(self.length_scale),
+               N.ptr(w_ceil), N.ptr(y_lengths), N.ptr(o_attn_dur), stream)
+        T_y = int(y_lengths.max().item())  # sequence_mask(y_lengths, None) (glow_tts.py:353)
+        noise = aux_input.get("noise")
+        if noise is not None:
+            noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+            if noise.shape != (B, C, T_y):
+                raise ValueError(f"noise must be [{B}, {C}, {T_y}], got {tuple(noise.shape)}")
+        elif self.inference_noise_scale != 0:
+            noise = torch.randn(B, C, T_y, device=dev)
+        z = torch.empty(B, C, T_y, device=dev)
+        y_mask = torch.empty(B, 1, T_y, device=dev)
+        y_mean = torch.empty(B, C, T_y, device=dev)
+        y_log_scale = torch.empty(B, C, T_y, device=dev)
+        attn = torch.empty(B, T_x, T_y, device=dev)
+        N.call("tts_glow_expand", N.ptr(w_ceil), N.ptr(x_mask), N.ptr(y_lengths), N.ptr(o_mean),
+               N.ptr(None if self.mean_only else o_log_scale), N.ptr(noise), float(self.inference_noise_scale),
+               B, C, T_x, T_y, N.ptr(z), N.ptr(y_mask), N.ptr(y_mean), N.ptr(y_log_scale), N.ptr(attn), stream)
+        y, logdet = self.decoder(z, y_mask, reverse=True)
+        return {
+            "model_outputs": y.transpose(1, 2),
+            "logdet": logdet,
+            "y_mean": y_mean.transpose(1, 2),
+            "y_log_scale": y_log_scale.transpose(1, 2),
+            "alignments": attn.permute(0, 2, 1),
+            "durations_log": o_dur_log.transpose(1, 2),
+            "total_durations_log": o_attn_dur.transpose(1, 2),
+        }
+
+    def store_inverse(self):  # glow_tts.py:519-520
+        self.decoder.store_inverse()
+
+    def load_checkpoint(self, config, checkpoint_path, eval=False, cache=False):  # glow_tts.py:522-530
+        state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        self.load_state_dict(state["model"] if "model" in state else state)
+        if eval:
+            self.eval()
+            self.store_inverse()
+            assert not self.training
+
+
+__all__ = ["Encoder", "GlowTTS"]
