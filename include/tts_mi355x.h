@@ -16,6 +16,8 @@
  *   Glow-TTS encoder   TTS/tts/layers/glow_tts/encoder.py (rel_pos_transformer)
  *       Encoder.__init__                 :83-141    -> tts_glow_encoder_create
  *       Encoder.forward                  :143-179   -> tts_glow_encoder_forward
+ *   TTS -> vocoder hand-off  TTS/utils/synthesizer.py:412-428 -> tts_mel_handoff
+ *   save_wav int16 scaling   TTS/utils/audio/numpy_transforms.py:430-447 -> tts_wav_to_int16
  *   Glow-TTS inference glue  TTS/tts/models/glow_tts.py
  *       GlowTTS.inference durations      :349-351   -> tts_glow_durations
  *       generate_path + compute_outputs + z :352-361 -> tts_glow_expand
@@ -262,6 +264,39 @@ int tts_glow_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t*
                     const float* d_o_mean, const float* d_o_log_scale, const float* d_noise, float noise_scale,
                     int B, int C, int T_x, int T_y, float* d_z, float* d_y_mask, float* d_y_mean,
                     float* d_y_log_scale, float* d_attn, void* hip_stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* TTS -> vocoder hand-off and the int16 wav writer                                       */
+/* ------------------------------------------------------------------------------------ */
+
+/* AudioProcessor normalisation fields (processor.py:259-336; BaseAudioConfig defaults
+ * shared_configs.py:126-154), as the Python values (they are rounded to fp32 where numpy
+ * would).  d_mel_mean / d_mel_scale: device fp64 [C] mel_scaler statistics (mean-var
+ * normalisation, processor.py:275-277 / :316-318), or NULL for range normalisation. */
+typedef struct TtsAudioNormCfg {
+  int signal_norm;     /* 0: identity */
+  int symmetric_norm;
+  int clip_norm;
+  double max_norm;
+  double min_level_db;
+  double ref_level_db;
+  const double* d_mel_mean;
+  const double* d_mel_scale;
+} TtsAudioNormCfg;
+
+/* Synthesizer hand-off (synthesizer.py:412-428), batched: out[B][C][T_out] =
+ * interpolate(vocoder_ap.normalize(tts_ap.denormalize(in))).  in: model_outputs [B][T][C]
+ * (time_major = 1) or [B][C][T].  T_out == T: no resampling; otherwise the time axis is resampled
+ * like interpolate_vocoder_input (vocoder/utils/generic_utils.py:11-29: bilinear,
+ * align_corners=False, recompute_scale_factor=True; pass T_out = floor(T * sr_voc / sr_tts)).
+ * denorm / norm may be NULL (identity). */
+int tts_mel_handoff(const float* d_in, int B, int T, int C, int time_major, const TtsAudioNormCfg* denorm,
+                    const TtsAudioNormCfg* norm, int T_out, float* d_out, void* hip_stream);
+/* save_wav scaling (numpy_transforms.py:436-438): out = int16(wav * (32767 / max(0.01, max|wav|)))
+ * per utterance.  wav [B][n] fp32; d_lengths [B] (int64, NULL = n) limits each utterance (samples
+ * beyond it are written as 0); d_scratch: B x uint32 of device memory. */
+int tts_wav_to_int16(const float* d_wav, int B, int64_t n, const int64_t* d_lengths, unsigned* d_scratch,
+                     int16_t* d_out, void* hip_stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* VITS flow: ResidualCouplingBlocks, reverse (TTS/tts/layers/vits/networks.py:169-232)     */

@@ -276,6 +276,8 @@ def main():
         return main_vits()
     if len(sys.argv) > 1 and sys.argv[1] == "glow_tts":
         return main_glow_tts()
+    if len(sys.argv) > 1 and sys.argv[1] == "handoff":
+        return main_handoff()
     HifiganGenerator, Decoder = import_reference()
     v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
@@ -333,6 +335,30 @@ def main_glow_tts():
                                 "hidden_channels_ffn": 192, "rel_attn_window_size": 4},
                 mean_only=False, use_prenet=False)
     glow_encoder_case(Encoder, "glow_encoder_rel_b2_t19", rcfg, seed=97, B=2, T=19, lengths=[19, 11], tok_seed=43)
+
+
+def main_handoff():
+    """G8: mel_scaler mean-var (de)normalisation through the reference's StandardScaler
+    (TTS/tts/utils/helpers.py:14-39, as AudioProcessor applies it at processor.py:277 / :318) and
+    interpolate_vocoder_input's F.interpolate call (vocoder/utils/generic_utils.py:24-27)."""
+    import_reference()
+    from TTS.tts.utils.helpers import StandardScaler
+
+    rng = np.random.default_rng(5)
+    mel = (rng.standard_normal((37, 80)) * 2).astype(np.float32)  # model_outputs[0]: [T, C]
+    mean = rng.standard_normal(80) * 3 - 5   # float64, like the stats file
+    std = np.exp(rng.standard_normal(80) * 0.3) * 2
+    sc = StandardScaler(mean, std)
+    den = sc.inverse_transform(mel.copy())     # denormalize: mel_scaler.inverse_transform(S.T).T on [C,T]^T
+    ren = sc.transform(den.copy())
+    spec = torch.tensor(den.T.copy()).unsqueeze(0).unsqueeze(0)
+    interp = torch.nn.functional.interpolate(spec, scale_factor=[1, 24000 / 22050], recompute_scale_factor=True,
+                                             mode="bilinear", align_corners=False).squeeze(0)[0].numpy()
+    meta = dict(kind="handoff", sr_tts=22050, sr_voc=24000)
+    path = os.path.join(HERE, "handoff_meanvar_t37.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), mel=mel, mean=mean, std=std, denorm_ref=den, renorm_ref=ren,
+                        interp_ref=interp)
+    print(f"wrote {path}: denorm {den.dtype} interp {interp.shape}")
 
 
 if __name__ == "__main__":

@@ -166,3 +166,22 @@ def test_glow_tts_glue_oracle_matches_reference(name, meta, arr):
     # ceil() margin: no duration of the fixture sits within 1e-3 of an integer, so an fp32
     # implementation that matches the encoder to ~1e-6 must reproduce w_ceil exactly
     assert meta["ceil_margin"] > 1e-3
+
+
+HANDOFF = goldens("handoff")
+
+
+@pytest.mark.parametrize("name,meta,arr", HANDOFF, ids=[g[0] for g in HANDOFF])
+def test_handoff_oracle_matches_reference(name, meta, arr):
+    from oracle import handoff_ref
+
+    a = dict(signal_norm=True, symmetric_norm=True, clip_norm=True, max_norm=4.0, min_level_db=-100, ref_level_db=20,
+             mel_mean=arr["mean"], mel_std=arr["std"])
+    den = handoff_ref.denormalize(arr["mel"].T, a).T
+    assert den.dtype == np.float32 and np.array_equal(den, arr["denorm_ref"])
+    ren = handoff_ref.normalize(den.T, a).T
+    assert np.array_equal(ren, arr["renorm_ref"])
+    # the resampled hand-off of interpolate_vocoder_input
+    out = handoff_ref.handoff(arr["mel"], dict(a, sample_rate=meta["sr_tts"]), dict(a, signal_norm=False,
+                                                                                   sample_rate=meta["sr_voc"]))
+    assert np.array_equal(out, arr["interp_ref"])

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "glow.hpp"
+#include "handoff.hpp"
 #include "hifigan.hpp"
 #include "text.hpp"
 #include "vits.hpp"
@@ -68,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 106; }
+int tts_abi_version(void) { return 107; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -238,6 +239,52 @@ int tts_glow_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t*
     a.C = C; a.T_x = T_x; a.T_y = T_y;
     a.z = d_z; a.y_mask = d_y_mask; a.y_mean = d_y_mean; a.y_log_scale = d_y_log_scale; a.attn = d_attn;
     tts::launch_expand(a, B, static_cast<hipStream_t>(hip_stream));
+    TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+// ----------------------------------------------------------------------------- hand-off / wav writer
+namespace {
+tts::AudioNormDev to_dev(const TtsAudioNormCfg* c) {
+  tts::AudioNormDev d{};
+  if (!c || !c->signal_norm) return d;  // signal_norm = 0: identity
+  TTS_REQUIRE((c->d_mel_mean == nullptr) == (c->d_mel_scale == nullptr), 1,
+              "mel_scaler needs both d_mel_mean and d_mel_scale");
+  d.signal_norm = 1;
+  d.symmetric_norm = c->symmetric_norm;
+  d.clip_norm = c->clip_norm;
+  d.max_norm = (float)c->max_norm;
+  d.two_max_norm = (float)(2.0 * c->max_norm);       // (2 * self.max_norm) in Python
+  d.min_level_db = (float)c->min_level_db;
+  d.neg_min_level_db = (float)(-c->min_level_db);   // -self.min_level_db in Python
+  d.ref_level_db = (float)c->ref_level_db;
+  d.mean = c->d_mel_mean;
+  d.scale = c->d_mel_scale;
+  return d;
+}
+}  // namespace
+
+int tts_mel_handoff(const float* d_in, int B, int T, int C, int time_major, const TtsAudioNormCfg* denorm,
+                    const TtsAudioNormCfg* norm, int T_out, float* d_out, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_in && d_out, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && T >= 1 && C >= 1 && T_out >= 1, 1, "bad hand-off shape");
+    TTS_REQUIRE(C <= 65535 && B <= 65535, 3, "hand-off: C and B must be <= 65535");
+    tts::HandoffArgs a{};
+    a.in = d_in; a.out = d_out; a.T = T; a.C = C; a.T_out = T_out; a.time_major = time_major ? 1 : 0;
+    a.de = to_dev(denorm);
+    a.no = to_dev(norm);
+    tts::launch_handoff(a, B, static_cast<hipStream_t>(hip_stream));
+    TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+int tts_wav_to_int16(const float* d_wav, int B, int64_t n, const int64_t* d_lengths, unsigned* d_scratch,
+                     int16_t* d_out, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_wav && d_scratch && d_out, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && B <= 65535 && n >= 1, 1, "bad wav shape");
+    tts::launch_wav_int16(d_wav, B, n, d_lengths, d_scratch, d_out, static_cast<hipStream_t>(hip_stream));
     TTS_HIP_CHECK(hipGetLastError());
   });
 }

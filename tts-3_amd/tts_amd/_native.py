@@ -87,6 +87,19 @@ class TtsGlowEncoderCfg(Structure):
     ]
 
 
+class TtsAudioNormCfg(Structure):
+    _fields_ = [
+        ("signal_norm", c_int),
+        ("symmetric_norm", c_int),
+        ("clip_norm", c_int),
+        ("max_norm", c_double),
+        ("min_level_db", c_double),
+        ("ref_level_db", c_double),
+        ("d_mel_mean", c_void_p),
+        ("d_mel_scale", c_void_p),
+    ]
+
+
 class TtsVitsFlowCfg(Structure):
     _fields_ = [
         ("channels", c_int),
@@ -178,6 +191,12 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int, c_int,
          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "tts_mel_handoff": (
+        c_int,
+        [c_void_p, c_int, c_int, c_int, c_int, POINTER(TtsAudioNormCfg), POINTER(TtsAudioNormCfg), c_int, c_void_p,
+         c_void_p],
+    ),
+    "tts_wav_to_int16": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tts_vits_flow_num_weights": (c_int, [POINTER(TtsVitsFlowCfg)]),
     "tts_vits_flow_weight_numel": (c_int64, [POINTER(TtsVitsFlowCfg), c_int]),
     "tts_vits_flow_create": (c_int, [POINTER(TtsVitsFlowCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
