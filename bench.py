@@ -67,6 +67,7 @@ def parse():
     p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
     p.add_argument("--no-glow", action="store_true", help="skip the Glow-TTS decoder measurement")
     p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
+    p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -241,6 +242,7 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
     (its durations are ceil()-quantised, so they must match the reference's)."""
     from tts_amd import synthetic
     from tts_amd.config import GLOW_TTS_DECODER as G, GLOW_TTS_ENCODER as E
+    from tts_amd.synthesizer import AudioNorm, Synthesizer
     from tts_amd.tts import GlowTTS
 
     ecfg = dict(E, num_chars=64)
@@ -253,8 +255,9 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
     sd.update({f"decoder.{k}": v for k, v in synthetic.glow_decoder_state_dict(**dcfg, seed=4321).items()})
     tok = synthetic.tokens(B, T_x, 64, seed=11).to(dev)
     lens = torch.full((B,), T_x, dtype=torch.int64, device=dev)
-    out = {"workload": f"Glow-TTS LJSpeech cfg + HiFiGAN-v1, [{B} x {T_x}] token ids -> waveform "
-                       "(encoder fp32, noise_scale 0, length_scale 1)", "variants": {}}
+    out = {"workload": f"Glow-TTS LJSpeech cfg + on-device hand-off (denormalize/normalize) + HiFiGAN-v1, "
+                       f"[{B} x {T_x}] token ids -> waveform (encoder fp32, noise_scale 0, length_scale 1)",
+           "variants": {}}
     for label, (dmode, vmode) in modes.items():
         m = GlowTTS(dict(num_chars=64), decoder_math_mode=dmode)
         m.load_state_dict(sd)
@@ -262,10 +265,10 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
         m.store_inverse()
         m = m.to(dev)
         voc = build_generator(vmode, dev)
+        syn = Synthesizer(m, voc, AudioNorm(), AudioNorm())  # BaseAudioConfig defaults both sides
 
         def step():
-            mel = m.inference(tok, {"x_lengths": lens})["model_outputs"].transpose(1, 2)
-            return voc.inference(mel)
+            return syn.tts_batch(tok, lens)[0]
 
         for _ in range(warmup):
             wav = step()
@@ -292,8 +295,39 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
             "glow_tts_inference_ms": ms_glow,
             "encoder_kernel_ms": sum(r["ms"] for r in erows), "encoder_launches": len(erows),
         }
-        del m, voc
+        del m, voc, syn
     return out
+
+
+def xtts_decoder_bench(dev, math_mode, steps=10, warmup=3, B=16, T=64):
+    """XTTS waveform decoder (HifiDecoder, xtts/hifigan_decoder.py:603-700): GPT latents [B, T, 1024]
+    -> linear resampling x4 and x24000/22050 -> HiFiGAN (1024 -> 512 ch, conds in every upsampling
+    layer) -> 24 kHz waveform."""
+    from tts_amd import synthetic
+    from tts_amd.tts import HifiDecoder
+
+    d = HifiDecoder(math_mode=math_mode)
+    cfg = dict(in_channels=1024, out_channels=1, resblock_type="1",
+               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+               upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=512, upsample_factors=[8, 8, 2, 2],
+               cond_channels=512, conv_pre_weight_norm=False, conv_post_weight_norm=False, conv_post_bias=False,
+               cond_in_each_up_layer=True)
+    d.waveform_decoder.load_state_dict(synthetic.hifigan_state_dict(**cfg, seed=321, weight_norm=True))
+    d.eval()
+    d = d.to(dev)
+    lat = torch.randn(B, T, 1024, generator=torch.Generator().manual_seed(1)).to(dev)
+    g = (torch.randn(B, 512, 1, generator=torch.Generator().manual_seed(2)) * 0.5).to(dev)
+    for _ in range(warmup):
+        wav = d.inference(lat, g)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        wav = d.inference(lat, g)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"workload": f"XTTS HifiDecoder, [{B} x {T}] GPT latents -> 24 kHz waveform ({wav.shape[2]} samples each)",
+            "math_mode": math_mode, "ms_per_step": ms, "samples_per_s": wav.numel() / (ms / 1e3),
+            "rtf": (ms / 1e3) / (wav.numel() / 24000)}
 
 
 def main():
@@ -388,6 +422,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_e2e:
         e2e = glow_tts_e2e_bench(dev, {"fp32_faithful": ("fp32x6", "f16x3"), "bf16": ("bf16", "bf16")})
 
+    xtts = None
+    if rank == 0 and world == 1 and not a.no_xtts:
+        xtts = xtts_decoder_bench(dev, a.math_mode)
+
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -432,6 +470,7 @@ def main():
             "alt_math_mode": alt,
             "glow_decoder": glow,
             "glow_tts_e2e": e2e,
+            "xtts_decoder": xtts,
             "accuracy_vs_fp64_oracle": acc,
         }
         if comm:

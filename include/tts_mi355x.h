@@ -109,6 +109,8 @@ typedef struct TtsHifiganCfg {
   int cond_channels;                    /* 0 = no cond_layer (:227-228) */
   int conv_post_bias;                   /* default 1 (:177) */
   int math_mode;                        /* TTS_MATH_FP32 (default), _X6, _F16X3 or TTS_MATH_BF16 */
+  int cond_in_each_up_layer;            /* XTTS generator (TTS/tts/layers/xtts/hifigan_decoder.py:199, :276-279):
+                                           o = ups[i](o) + conds[i](g) after every upsampling; needs cond_channels */
 } TtsHifiganCfg;
 
 /* Number of host weight tensors create() expects, and the element count of tensor idx.
@@ -120,6 +122,8 @@ typedef struct TtsHifiganCfg {
  *       type 2: convs.m.weight/bias for m < num_dilations
  *   conv_post.weight [out][C_last][7], conv_post.bias [out] (only if conv_post_bias)
  *   cond_layer.weight [C0][cond][1], cond_layer.bias [C0]  (only if cond_channels > 0)
+ *   conds.i.weight [C_{i+1}][cond][1], conds.i.bias [C_{i+1}] for i < num_upsamples
+ *                                                          (only if cond_in_each_up_layer)
  * with C0 = upsample_initial_channel, C_i = C0 >> i. */
 int tts_hifigan_num_weights(const TtsHifiganCfg* cfg);
 int64_t tts_hifigan_weight_numel(const TtsHifiganCfg* cfg, int idx);
@@ -288,10 +292,13 @@ typedef struct TtsAudioNormCfg {
  * interpolate(vocoder_ap.normalize(tts_ap.denormalize(in))).  in: model_outputs [B][T][C]
  * (time_major = 1) or [B][C][T].  T_out == T: no resampling; otherwise the time axis is resampled
  * like interpolate_vocoder_input (vocoder/utils/generic_utils.py:11-29: bilinear,
- * align_corners=False, recompute_scale_factor=True; pass T_out = floor(T * sr_voc / sr_tts)).
- * denorm / norm may be NULL (identity). */
+ * align_corners=False, recompute_scale_factor=True; pass T_out = floor(T * sr_voc / sr_tts) and
+ * src_scale = 0, which maps with T / T_out).  src_scale > 0 maps output j to source
+ * src_scale * (j + 0.5) - 0.5 instead: F.interpolate(mode="linear", scale_factor=s) without
+ * recompute_scale_factor passes src_scale = 1/s (the XTTS latent upsampling,
+ * xtts/hifigan_decoder.py:688-698).  denorm / norm may be NULL (identity). */
 int tts_mel_handoff(const float* d_in, int B, int T, int C, int time_major, const TtsAudioNormCfg* denorm,
-                    const TtsAudioNormCfg* norm, int T_out, float* d_out, void* hip_stream);
+                    const TtsAudioNormCfg* norm, int T_out, float src_scale, float* d_out, void* hip_stream);
 /* save_wav scaling (numpy_transforms.py:436-438): out = int16(wav * (32767 / max(0.01, max|wav|)))
  * per utterance.  wav [B][n] fp32; d_lengths [B] (int64, NULL = n) limits each utterance (samples
  * beyond it are written as 0); d_scratch: B x uint32 of device memory. */

@@ -14,6 +14,8 @@ tolerance gates).  It follows, line by line, Coqui TTS 0.22.0:
                 slope 0.01) -> conv_post -> tanh
 * ``:267-282``  inference: replicate pad of inference_padding frames on both sides
 * ``:284-291``  remove_weight_norm: w = g * v / ||v|| with the norm over all dims but 0
+* ``TTS/tts/layers/xtts/hifigan_decoder.py:240-244, :276-279``  the XTTS generator's
+  cond_in_each_up_layer: o = ups[i](o) + conds[i](g)
 
 Pinned against golden vectors produced by the reference module itself
 (tests/golden/make_goldens.py, checked by tests/test_oracle_golden.py).
@@ -83,6 +85,8 @@ def hifigan_forward(
     for i, (u, k) in enumerate(zip(upsample_factors, upsample_kernel_sizes)):
         o = F.leaky_relu(o, LRELU_SLOPE)  # :253
         o = F.conv_transpose1d(o, w[f"ups.{i}.weight"], w[f"ups.{i}.bias"], stride=u, padding=(k - u) // 2)
+        if f"conds.{i}.weight" in w:  # XTTS cond_in_each_up_layer (xtts/hifigan_decoder.py:276-279)
+            o = o + F.conv1d(g.to(dtype), w[f"conds.{i}.weight"], w[f"conds.{i}.bias"])
         stages[f"ups.{i}"] = o
         z_sum = None
         for j, (kk, dil) in enumerate(zip(resblock_kernel_sizes, resblock_dilation_sizes)):

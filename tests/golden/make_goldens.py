@@ -278,6 +278,8 @@ def main():
         return main_glow_tts()
     if len(sys.argv) > 1 and sys.argv[1] == "handoff":
         return main_handoff()
+    if len(sys.argv) > 1 and sys.argv[1] == "xtts":
+        return main_xtts()
     HifiganGenerator, Decoder = import_reference()
     v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
@@ -335,6 +337,55 @@ def main_glow_tts():
                                 "hidden_channels_ffn": 192, "rel_attn_window_size": 4},
                 mean_only=False, use_prenet=False)
     glow_encoder_case(Encoder, "glow_encoder_rel_b2_t19", rcfg, seed=97, B=2, T=19, lengths=[19, 11], tok_seed=43)
+
+
+def main_xtts():
+    """G9: the XTTS waveform decoder (TTS/tts/layers/xtts/hifigan_decoder.py HifiDecoder.forward :688-700
+    around its HifiganGenerator with cond_in_each_up_layer).  That module imports torchaudio (absent),
+    so the reference's vocoder HifiganGenerator (identical except for the per-layer conditioning) runs
+    the network, and forward hooks on ups[i] add conds[i](g) exactly where the XTTS forward does
+    (:276-279); the two latent interpolations are the reference's F.interpolate calls."""
+    HifiganGenerator, _ = import_reference()
+    cfg = dict(in_channels=1024, out_channels=1, resblock_type="1",
+               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+               upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=512, upsample_factors=[8, 8, 2, 2],
+               inference_padding=0, cond_channels=512, conv_pre_weight_norm=False, conv_post_weight_norm=False,
+               conv_post_bias=False, cond_in_each_up_layer=True)
+    seed, B, T = 321, 2, 6
+    torch.manual_seed(0)
+    ref = HifiganGenerator(**{k: v for k, v in cfg.items() if k != "cond_in_each_up_layer"})
+    sd = synthetic.hifigan_state_dict(**cfg, seed=seed, weight_norm=True)
+    conds = {k: v for k, v in sd.items() if k.startswith("conds.")}
+    ref.load_state_dict({k: v for k, v in sd.items() if not k.startswith("conds.")})
+    ref.eval()
+    gen = torch.Generator().manual_seed(17)
+    latents = torch.randn(B, T, 1024, generator=gen)  # GPT latents [B, T, C]
+    g = torch.randn(B, 512, 1, generator=gen) * 0.5
+
+    def run(model, dtype):
+        gg = g.to(dtype)
+        hooks = [u.register_forward_hook(
+            lambda m, inp, o, i=i: o + torch.nn.functional.conv1d(gg, conds[f"conds.{i}.weight"].to(dtype),
+                                                                  conds[f"conds.{i}.bias"].to(dtype)))
+            for i, u in enumerate(model.ups)]
+        with torch.no_grad():
+            z = torch.nn.functional.interpolate(latents.to(dtype).transpose(1, 2), scale_factor=[1024 / 256],
+                                                mode="linear").squeeze(1)
+            z = torch.nn.functional.interpolate(z, scale_factor=[24000 / 22050], mode="linear").squeeze(0)
+            out = model.forward(z, gg)
+        for h in hooks:
+            h.remove()
+        return z, out
+
+    z32, o32 = run(ref, torch.float32)
+    z64, o64 = run(ref.double(), torch.float64)
+    meta = dict(kind="xtts_decoder", config=cfg, seed=seed, B=B, T=T, input_sample_rate=22050,
+                output_sample_rate=24000, output_hop_length=256, ar_mel_length_compression=1024)
+    path = os.path.join(HERE, "xtts_decoder_b2_t6.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), latents=latents.numpy(), g=g.numpy(), z_ref_fp32=z32.numpy(),
+                        z_ref_fp64=z64.numpy(), out_ref_fp32=o32.numpy(), out_ref_fp64=o64.numpy())
+    print(f"wrote {path}: z {tuple(z32.shape)} out {tuple(o32.shape)} std {o32.std():.4f} "
+          f"max|fp32-fp64| {np.abs(o32.numpy() - o64.numpy()).max():.2e}")
 
 
 def main_handoff():

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 107
+    assert N.lib().tts_abi_version() == 108
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -269,3 +269,20 @@ def test_glow_tts_config_defaults_follow_reference():
     keys = set(m.state_dict())
     assert "encoder.encoder.attn_layers.5.conv_o.weight" in keys
     assert "decoder.flows.35.wn.res_skip_layers.3.parametrizations.weight.original1" in keys
+
+
+def test_xtts_generator_inventory_and_validation():
+    cfg = dict(in_channels=1024, out_channels=1, resblock_type="1",
+               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+               upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=512, upsample_factors=[8, 8, 2, 2],
+               inference_padding=0, cond_channels=512, conv_pre_weight_norm=False, conv_post_weight_norm=False,
+               conv_post_bias=False)
+    g = HifiganGenerator(**cfg, cond_in_each_up_layer=True)
+    sd = synthetic.hifigan_state_dict(**cfg, cond_in_each_up_layer=True, seed=1)
+    g.load_state_dict(sd)  # strict: conds.* keys as the XTTS module
+    ws = g._weight_list()
+    assert len(ws) == N.lib().tts_hifigan_num_weights(ctypes.byref(g._cfg)) == 2 + 8 + 144 + 1 + 2 + 8
+    for i, w in enumerate(ws):
+        assert N.lib().tts_hifigan_weight_numel(ctypes.byref(g._cfg), i) == w.size
+    with pytest.raises(N.NativeError):
+        HifiganGenerator(**dict(cfg, cond_channels=0), cond_in_each_up_layer=True)

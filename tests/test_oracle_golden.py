@@ -185,3 +185,16 @@ def test_handoff_oracle_matches_reference(name, meta, arr):
     out = handoff_ref.handoff(arr["mel"], dict(a, sample_rate=meta["sr_tts"]), dict(a, signal_norm=False,
                                                                                    sample_rate=meta["sr_voc"]))
     assert np.array_equal(out, arr["interp_ref"])
+
+
+XTTS = goldens("xtts_decoder")
+
+
+@pytest.mark.parametrize("name,meta,arr", XTTS, ids=[g[0] for g in XTTS])
+def test_xtts_decoder_oracle_matches_reference(name, meta, arr):
+    cfg = meta["config"]
+    sd = synthetic.hifigan_state_dict(**cfg, seed=meta["seed"], weight_norm=True)
+    z = torch.from_numpy(arr["z_ref_fp64"])
+    out = hifigan_ref.hifigan_forward(sd, z, pad=0, g=torch.from_numpy(arr["g"]), dtype=torch.float64,
+                                      fold_dtype=torch.float64, **cfg)
+    assert max_abs(out.numpy(), arr["out_ref_fp64"]) < 1e-10

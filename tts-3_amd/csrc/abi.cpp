@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 107; }
+int tts_abi_version(void) { return 108; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -265,13 +265,14 @@ tts::AudioNormDev to_dev(const TtsAudioNormCfg* c) {
 }  // namespace
 
 int tts_mel_handoff(const float* d_in, int B, int T, int C, int time_major, const TtsAudioNormCfg* denorm,
-                    const TtsAudioNormCfg* norm, int T_out, float* d_out, void* hip_stream) {
+                    const TtsAudioNormCfg* norm, int T_out, float src_scale, float* d_out, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(d_in && d_out, 1, "NULL argument");
     TTS_REQUIRE(B >= 1 && T >= 1 && C >= 1 && T_out >= 1, 1, "bad hand-off shape");
     TTS_REQUIRE(C <= 65535 && B <= 65535, 3, "hand-off: C and B must be <= 65535");
     tts::HandoffArgs a{};
     a.in = d_in; a.out = d_out; a.T = T; a.C = C; a.T_out = T_out; a.time_major = time_major ? 1 : 0;
+    a.src_scale = src_scale;
     a.de = to_dev(denorm);
     a.no = to_dev(norm);
     tts::launch_handoff(a, B, static_cast<hipStream_t>(hip_stream));

@@ -61,7 +61,8 @@ struct Conv1dArgs {
   // ups = U > 0 (split kernels, K = 2): polyphase ConvTranspose1d(kernel 2U, stride U, padding
   // U/2).  Rows are rho = co*U + s (Cout = U * channels), columns are frames m in [0, Tin]
   // (Tout = Tin + 1, pad = 1: taps x[m-1], x[m]); row rho, column m is stored at time
-  // U*m + s - U/2 of y[b][co][0 .. U*Tin).  zmode 0, no res / mask / cvec.
+  // U*m + s - U/2 of y[b][co][0 .. U*Tin).  zmode 0, no res / mask; cvec [B][channels] is
+  // added after the bias (channel co = rho / U).
   int ups;
   int64_t o_bstride;     // floats between batch items of res / y / z (0 = Cout*Tout)
   int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
@@ -96,6 +97,7 @@ struct ConvTArgs {
   int n_chunks;
   float in_slope;
   unsigned* amax_out;  // [B][64] slots receiving max |y[b]| (fp32 bits), or nullptr
+  const float* cvec;   // [B][Cout] added after the bias (XTTS conds[i](g)), or nullptr
 };
 
 struct PostArgs {

@@ -138,14 +138,17 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
   const unsigned plane = (unsigned)Cr * (unsigned)To * 4u;
   const rsrc_t rout = make_rsrc(a.y + (size_t)b * Cr * To, plane);
   const rsrc_t rbias = make_rsrc(a.bias, (unsigned)a.Cout * 4u);
+  // cvec: 0 records when absent, so every read returns 0 and (acc + bias) + 0 is exact
+  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * Cr : a.bias, a.cvec ? (unsigned)Cr * 4u : 0u);
   float vmax = 0.f;
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
-    float bv[16];
+    float bv[16], cv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned rho = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
       bv[r] = bload(rbias, rho * 4u, 0u);
+      cv[r] = bload(rcv, (rho >> lgU) * 4u, 0u);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
@@ -157,7 +160,7 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
         const int t = (mm << lgU) + (rho & (U - 1)) - (U >> 1);
         // rows >= Cout land past the plane (co >= Cr); samples outside [0, To) are marked OOB
         const unsigned off = (t >= 0 && t < To) ? ((unsigned)co * (unsigned)To + (unsigned)t) * 4u : OOB_OFF;
-        const float v = acc[m][n][r] + bv[r];
+        const float v = (acc[m][n][r] + bv[r]) + cv[r];
         if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v));
         bstore(rout, v, off, 0u);
       }

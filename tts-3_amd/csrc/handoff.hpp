@@ -22,6 +22,7 @@ struct HandoffArgs {
   const float* in;  // [B][T][C] (time_major) or [B][C][T]
   float* out;       // [B][C][T_out]
   int T, C, T_out, time_major;
+  float src_scale;  // > 0: source step per output step (1 / scale_factor); else T / T_out
   AudioNormDev de, no;
 };
 

@@ -45,6 +45,12 @@ std::vector<int64_t> hifigan_weight_shapes(const TtsHifiganCfg& c) {
     n.push_back((int64_t)C0 * c.cond_channels);
     n.push_back(C0);
   }
+  if (c.cond_in_each_up_layer) {
+    for (int i = 0; i < c.num_upsamples; ++i) {
+      n.push_back((int64_t)(C0 >> (i + 1)) * c.cond_channels);
+      n.push_back(C0 >> (i + 1));
+    }
+  }
   return n;
 }
 
@@ -78,6 +84,7 @@ void hifigan_validate(const TtsHifiganCfg& c) {
   }
   TTS_REQUIRE(c.inference_padding >= 0, 1, "inference_padding must be >= 0");
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
+  TTS_REQUIRE(!c.cond_in_each_up_layer || c.cond_channels > 0, 1, "cond_in_each_up_layer needs cond_channels > 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
 }
 
@@ -179,6 +186,9 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   if (cfg_.conv_post_bias) wi += 1;
   const float* cond_w = nullptr; const float* cond_b = nullptr;
   if (cfg_.cond_channels > 0) { cond_w = hw[wi]; cond_b = hw[wi + 1]; wi += 2; }
+  std::vector<std::pair<const float*, const float*>> upcond;  // conds.i (XTTS)
+  if (cfg_.cond_in_each_up_layer)
+    for (int i = 0; i < cfg_.num_upsamples; ++i) { upcond.push_back({hw[wi], hw[wi + 1]}); wi += 2; }
 
   // arena layout
   std::vector<ConvLayer*> convs;
@@ -191,6 +201,8 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const int Cl = C0 >> cfg_.num_upsamples;
   total += align((int64_t)Cl * 7);
   if (cfg_.cond_channels > 0) total += align((int64_t)C0 * cfg_.cond_channels) + align(C0);
+  for (size_t i = 0; i < upcond.size(); ++i)
+    total += align((int64_t)(C0 >> (i + 1)) * cfg_.cond_channels) + align(C0 >> (i + 1));
 
   std::vector<float> host(total, 0.f);
   int64_t off = 0;
@@ -234,6 +246,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     std::memcpy(host.data() + off, cond_b, sizeof(float) * C0);
     cond_b_off = off; off += align(C0);
   }
+  std::vector<std::pair<int64_t, int64_t>> upcond_off;
+  for (size_t i = 0; i < upcond.size(); ++i) {
+    const int64_t ci = C0 >> (i + 1);
+    std::memcpy(host.data() + off, upcond[i].first, sizeof(float) * ci * cfg_.cond_channels);
+    const int64_t wo = off; off += align(ci * cfg_.cond_channels);
+    std::memcpy(host.data() + off, upcond[i].second, sizeof(float) * ci);
+    upcond_off.push_back({wo, off}); off += align(ci);
+  }
 
   weights_bytes_ = (size_t)total * sizeof(float);
   if (hipMalloc(&arena_, weights_bytes_) != hipSuccess) throw Error(4, "hipMalloc(weights) failed");
@@ -243,6 +263,7 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   for (auto& u : ups_) { u.w = arena_ + offs[oi++]; u.b = arena_ + offs[oi++]; }
   post_wd_ = arena_ + post_off;
   if (cfg_.cond_channels > 0) { cond_wd_ = arena_ + cond_w_off; cond_bd_ = arena_ + cond_b_off; }
+  for (auto& o : upcond_off) up_cond_.push_back({arena_ + o.first, arena_ + o.second});
   hop_ = 1;
   for (int i = 0; i < cfg_.num_upsamples; ++i) hop_ *= cfg_.upsample_factors[i];
 }
@@ -274,8 +295,18 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
 int Hifigan::amax_groups() const { return 2 + cfg_.num_upsamples * (2 + cfg_.num_kernels * 6); }
 int Hifigan::stage_group(int i) const { return 2 + i * (2 + cfg_.num_kernels * 6); }
 
+int64_t Hifigan::cond_floats(int B) const {
+  // cond_layer(g) [B][C0], then (XTTS) conds[i](g) [B][C_{i+1}] per stage
+  if (cfg_.cond_channels <= 0) return 0;
+  int64_t n = (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64;
+  if (cfg_.cond_in_each_up_layer)
+    for (int i = 0; i < cfg_.num_upsamples; ++i)
+      n += (((int64_t)B * (cfg_.upsample_initial_channel >> (i + 1)) + 63) / 64) * 64;
+  return n;
+}
+
 int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
-  const int64_t cond = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
+  const int64_t cond = cond_floats(B);
   const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
   return (4 * plane_floats(B, T, pad) + cond + amax) * (int64_t)sizeof(float);
 }
@@ -307,9 +338,8 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   float* bufX = ws_ + 2 * plane;  // resblock running residual x
   float* bufT = ws_ + 3 * plane;  // convs1 output (already leaky-relu'd)
   float* cvec = cfg_.cond_channels > 0 ? ws_ + 4 * plane : nullptr;
-  const int64_t cond_floats = cfg_.cond_channels > 0 ? (((int64_t)B * cfg_.upsample_initial_channel + 63) / 64) * 64 : 0;
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
-  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + 4 * plane + cond_floats) : nullptr;
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + 4 * plane + cond_floats(B)) : nullptr;
   auto slots = [&](int grp) -> unsigned* { return amax ? amax + (size_t)grp * B * 64 : nullptr; };  // [B][64]
   if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, (size_t)amax_groups() * B * 64 * sizeof(unsigned), s));
 
@@ -344,9 +374,18 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
 
   int len = L;
   const float* cur = bufZ;
+  float* upvec = cvec ? cvec + (((int64_t)B * C0 + 63) / 64) * 64 : nullptr;  // conds[i](g), XTTS
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
     const ConvTLayer& U = ups_[i];
-    const int g0 = stage_group(i);  // this stage's slot groups: o, per conv, z
+    const int g0 = stage_group(i);
+    const float* ucv = nullptr;  // o = ups[i](o) + conds[i](g) (xtts/hifigan_decoder.py:276-279)
+    if (cfg_.cond_in_each_up_layer) {
+      const int ci = U.Cout;
+      run(prof, s, "cond_up", 2.0 * B * ci * cfg_.cond_channels, 4.0 * (B * cfg_.cond_channels + ci * cfg_.cond_channels + B * ci),
+          [&] { launch_cond_vec(gvec, up_cond_[i].first, up_cond_[i].second, upvec, B, cfg_.cond_channels, ci, s); });
+      ucv = upvec;
+      upvec += (((int64_t)B * ci + 63) / 64) * 64;
+    }  // this stage's slot groups: o, per conv, z
     const unsigned* z_amax = slots(i == 0 ? 1 : stage_group(i - 1) + 1 + cfg_.num_kernels * 6);
     const int lout = len * U.U;
     const double uflops = 2.0 * B * U.Cout * (double)U.Cin * 2 * lout;
@@ -358,11 +397,13 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
       a.dil = 1; a.pad = 1; a.n_chunks = U.n_chunks;
       a.in_slope = 0.1f; a.out_slope = 1.f; a.zdiv = 1.f;
       a.amax_in = z_amax; a.amax_out = slots(g0); a.w_exp = U.w_exp; a.ups = U.U;
+      a.cvec = ucv;
       run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_conv(U.mode, a, B, 2, U.tile, s); });
     } else {
       ConvTArgs ta{};
       ta.x = cur; ta.w = U.w; ta.bias = U.b; ta.y = bufO;
       ta.Cin = U.Cin; ta.Cout = U.Cout; ta.Tin = len; ta.n_chunks = U.n_chunks; ta.in_slope = 0.1f;
+      ta.cvec = ucv;
       run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_convT(ta, B, U.U, U.tile, s); });
     }
     len = lout;

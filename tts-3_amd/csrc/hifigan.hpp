@@ -96,6 +96,7 @@ class Hifigan {
   };
 
   int64_t plane_floats(int B, int T, int pad) const;
+  int64_t cond_floats(int B) const;
   int amax_groups() const;
   int stage_group(int i) const;
 
@@ -110,6 +111,7 @@ class Hifigan {
   float* post_wd_ = nullptr;
   float* cond_wd_ = nullptr;
   float* cond_bd_ = nullptr;
+  std::vector<std::pair<float*, float*>> up_cond_;  // conds.i (w [C_i][cond], b [C_i]), XTTS
   float* arena_ = nullptr;
   size_t weights_bytes_ = 0;
   float* ws_ = nullptr;

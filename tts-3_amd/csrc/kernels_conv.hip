@@ -353,18 +353,19 @@ __global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
         const int co = mt * BM + wm * TM * 32 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
         if (co >= Cout || mm > Tin) continue;
         const float bb = a.bias[co];
+        const float cc = a.cvec ? a.cvec[(size_t)b * Cout + co] : 0.f;  // XTTS conds[i](g)
         float* yrow = a.y + ((size_t)b * Cout + co) * Tout;
         if constexpr (U == 8) {
           // phases 0..3 -> t = 8mm-4 .. 8mm-1 ; phases 4..7 -> t = 8mm .. 8mm+3
           if (mm >= 1) {
-            f32x4 v = {acc[0][m][n][r] + bb, acc[1][m][n][r] + bb, acc[2][m][n][r] + bb,
-                       acc[3][m][n][r] + bb};
+            f32x4 v = {acc[0][m][n][r] + bb + cc, acc[1][m][n][r] + bb + cc, acc[2][m][n][r] + bb + cc,
+                       acc[3][m][n][r] + bb + cc};
             vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             *reinterpret_cast<f32x4*>(yrow + 8 * mm - 4) = v;
           }
           if (mm < Tin) {
-            f32x4 v = {acc[4][m][n][r] + bb, acc[5][m][n][r] + bb, acc[6][m][n][r] + bb,
-                       acc[7][m][n][r] + bb};
+            f32x4 v = {acc[4][m][n][r] + bb + cc, acc[5][m][n][r] + bb + cc, acc[6][m][n][r] + bb + cc,
+                       acc[7][m][n][r] + bb + cc};
             vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
             *reinterpret_cast<f32x4*>(yrow + 8 * mm) = v;
           }
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
           for (int s = 0; s < U; ++s) {
             const int t = U * mm + s - P;
             if (t >= 0 && t < Tout) {
-              const float v = acc[s][m][n][r] + bb;
+              const float v = acc[s][m][n][r] + bb + cc;
               vmax = fmaxf(vmax, fabsf(v));
               yrow[t] = v;
             }

@@ -111,7 +111,7 @@ int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res)
 void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
   TTS_REQUIRE((K == 2) == (a.ups > 0), 1, "conv1d(split): K == 2 is the ConvTranspose1d form (ups > 0)");
   TTS_REQUIRE(a.ups == 0 || ((a.ups & (a.ups - 1)) == 0 && a.Cout % a.ups == 0 && a.zmode == 0 && !a.res &&
-                             !a.mask && !a.cvec && a.Tout == a.Tin + 1 && a.pad == 1),
+                             !a.mask && a.Tout == a.Tin + 1 && a.pad == 1),
               1, "conv1d(split): bad ConvTranspose1d arguments");
   // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,

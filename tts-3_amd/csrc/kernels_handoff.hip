@@ -74,7 +74,8 @@ __global__ void __launch_bounds__(256) handoff_kernel(HandoffArgs a) {
     y = load(j);
   } else {
     // PyTorch upsample_linear: src = scale * (j + 0.5) - 0.5, clamped at 0; scale = T / T_out
-    const float scale = (float)T / (float)a.T_out;
+    // (recompute_scale_factor=True) or 1 / scale_factor as given (a.src_scale > 0)
+    const float scale = a.src_scale > 0.f ? a.src_scale : (float)T / (float)a.T_out;
     float src = scale * ((float)j + 0.5f) - 0.5f;
     src = src < 0.f ? 0.f : src;
     const int i0 = (int)src;

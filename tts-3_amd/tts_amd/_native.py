@@ -50,6 +50,7 @@ class TtsHifiganCfg(Structure):
         ("cond_channels", c_int),
         ("conv_post_bias", c_int),
         ("math_mode", c_int),
+        ("cond_in_each_up_layer", c_int),
     ]
 
 
@@ -193,8 +194,8 @@ SIGNATURES = {
     ),
     "tts_mel_handoff": (
         c_int,
-        [c_void_p, c_int, c_int, c_int, c_int, POINTER(TtsAudioNormCfg), POINTER(TtsAudioNormCfg), c_int, c_void_p,
-         c_void_p],
+        [c_void_p, c_int, c_int, c_int, c_int, POINTER(TtsAudioNormCfg), POINTER(TtsAudioNormCfg), c_int, c_float,
+         c_void_p, c_void_p],
     ),
     "tts_wav_to_int16": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "tts_vits_flow_num_weights": (c_int, [POINTER(TtsVitsFlowCfg)]),

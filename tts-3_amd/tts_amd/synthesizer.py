@@ -66,8 +66,10 @@ class AudioNorm:
 
 
 def mel_handoff(model_outputs: torch.Tensor, tts_audio: Optional[AudioNorm], vocoder_audio: Optional[AudioNorm],
-                time_major: bool = True) -> torch.Tensor:
-    """synthesizer.py:414-428 for a batch: [B, T, C] (time_major) or [B, C, T] -> vocoder input [B, C, T']."""
+                time_major: bool = True, scale_factor: Optional[float] = None) -> torch.Tensor:
+    """synthesizer.py:414-428 for a batch: [B, T, C] (time_major) or [B, C, T] -> vocoder input [B, C, T'].
+    ``scale_factor``: resample the time axis like F.interpolate(mode="linear", scale_factor=...) (no
+    recompute_scale_factor), e.g. the XTTS latent upsampling; overrides the sample-rate rule."""
     N.require_device_tensor(model_outputs, "model_outputs")
     x = model_outputs.to(torch.float32).contiguous()
     if time_major:
@@ -78,12 +80,16 @@ def mel_handoff(model_outputs: torch.Tensor, tts_audio: Optional[AudioNorm], voc
     if tts_audio is not None and vocoder_audio is not None and vocoder_audio.sample_rate != tts_audio.sample_rate:
         # interpolate_vocoder_input (vocoder/utils/generic_utils.py:24-27): output size floor(T * scale)
         T_out = int(math.floor(T * (vocoder_audio.sample_rate / tts_audio.sample_rate)))
+    src_scale = 0.0
+    if scale_factor is not None:
+        T_out = int(math.floor(T * float(scale_factor)))
+        src_scale = 1.0 / float(scale_factor)
     dev = x.device
     de, k1 = tts_audio._native(dev) if tts_audio is not None else (None, [])
     no, k2 = vocoder_audio._native(dev) if vocoder_audio is not None else (None, [])
     out = torch.empty(B, C, T_out, device=dev)
     N.call("tts_mel_handoff", N.ptr(x), B, T, C, 1 if time_major else 0, ctypes.byref(de) if de else None,
-           ctypes.byref(no) if no else None, T_out, N.ptr(out), N.stream_ptr(dev))
+           ctypes.byref(no) if no else None, T_out, src_scale, N.ptr(out), N.stream_ptr(dev))
     del k1, k2  # the statistics are read by the kernel before the stream moves on (stream-ordered frees)
     return out
 

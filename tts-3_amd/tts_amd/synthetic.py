@@ -48,9 +48,11 @@ def hifigan_state_dict(
     conv_post_bias: bool = True,
     seed: int = 1234,
     weight_norm: bool = True,
+    cond_in_each_up_layer: bool = False,
     **_unused,
 ) -> "OrderedDict[str, torch.Tensor]":
-    """State dict of a HifiganGenerator (hifigan_generator.py:163-234) with synthetic weights.
+    """State dict of a HifiganGenerator (hifigan_generator.py:163-234) with synthetic weights
+    (``cond_in_each_up_layer``: the XTTS generator's ``conds.i``, xtts/hifigan_decoder.py:240-244).
 
     ``weight_norm=True`` gives the training-time parametrized keys; ``False`` gives the keys
     after ``remove_weight_norm`` (plain ``.weight``).
@@ -110,7 +112,13 @@ def hifigan_state_dict(
         w = rng.standard_normal((C0, cond_channels, 1)) / np.sqrt(cond_channels)
         sd["cond_layer.weight"] = torch.from_numpy(w.astype(np.float32))
         sd["cond_layer.bias"] = torch.from_numpy((rng.standard_normal((C0,)) * 0.01).astype(np.float32))
-    # canonical module order: conv_pre, ups, resblocks, conv_post, cond_layer
+    if cond_in_each_up_layer:
+        for i in range(len(upsample_factors)):
+            ci = C0 >> (i + 1)
+            w = rng.standard_normal((ci, cond_channels, 1)) * (0.3 / np.sqrt(cond_channels))
+            sd[f"conds.{i}.weight"] = torch.from_numpy(w.astype(np.float32))
+            sd[f"conds.{i}.bias"] = torch.from_numpy((rng.standard_normal((ci,)) * 0.01).astype(np.float32))
+    # canonical module order: conv_pre, ups, resblocks, conv_post, cond_layer, conds
     return sd
 
 

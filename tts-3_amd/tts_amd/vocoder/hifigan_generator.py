@@ -110,11 +110,14 @@ class HifiganGenerator(nn.Module):
         conv_post_weight_norm: bool = True,
         conv_post_bias: bool = True,
         math_mode: str = "fp32",
+        cond_in_each_up_layer: bool = False,
     ):
         """Arguments as the reference (:163-178).  ``math_mode`` selects how the conv contractions
         run on MI355X: ``"fp32"`` (v_mfma_f32_32x32x2_f32) or ``"fp32x6"`` (fp32 operands split
         exactly into 3 bf16 pieces, 6 cross products accumulated in fp32 on the bf16 matrix
-        cores; fp32-faithful, see include/tts_mi355x.h)."""
+        cores; fp32-faithful, see include/tts_mi355x.h).  ``cond_in_each_up_layer`` is the XTTS
+        generator's option (TTS/tts/layers/xtts/hifigan_decoder.py:199, :240-244, :276-279):
+        ``o = ups[i](o) + conds[i](g)`` after every upsampling."""
         super().__init__()
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
@@ -147,6 +150,8 @@ class HifiganGenerator(nn.Module):
         c.cond_channels = cond_channels
         c.conv_post_bias = 1 if conv_post_bias else 0
         c.math_mode = N.MATH_MODES[math_mode]
+        c.cond_in_each_up_layer = 1 if cond_in_each_up_layer else 0
+        self.cond_in_each_up_layer = cond_in_each_up_layer
         self.hop_length = int(np.prod(upsample_factors))
 
         # parameter tree identical to the reference (:203-234)
@@ -177,6 +182,11 @@ class HifiganGenerator(nn.Module):
             remove_parametrizations(self.conv_pre, "weight")
         if not conv_post_weight_norm:
             remove_parametrizations(self.conv_post, "weight")
+        if cond_in_each_up_layer:  # xtts/hifigan_decoder.py:240-244
+            self.conds = nn.ModuleList()
+            for i in range(len(self.ups)):
+                ch = upsample_initial_channel // (2 ** (i + 1))
+                self.conds.append(nn.Conv1d(cond_channels, ch, 1))
 
         self._handle = None
         self._handle_key = None
@@ -199,6 +209,9 @@ class HifiganGenerator(nn.Module):
             ws.append(_host(self.conv_post.bias))
         if hasattr(self, "cond_layer"):
             ws += [_effective_weight(self.cond_layer), _host(self.cond_layer.bias)]
+        if self.cond_in_each_up_layer:
+            for cv in self.conds:
+                ws += [_effective_weight(cv), _host(cv.bias)]
         return ws
 
     def _param_key(self):
