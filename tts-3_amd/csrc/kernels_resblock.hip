@@ -13,32 +13,50 @@
 // f16x3: xt's scale is the workgroup's own power of two (block max-abs): every conv2 output sums
 // products of one workgroup's xt only, so the per-tile scale is exact and batch-invariant.
 // The residual x is re-read from global memory, so x and x' must not alias (ping-pong buffers).
+#include <cstdlib>
+
 #include "split_device.hpp"
 
 namespace tts {
 
-constexpr int RP_W = 256;    // convs1 columns per workgroup
-constexpr int RP_BN = 224;   // output columns per workgroup
 constexpr int RP_LEAD = 16;  // xt row 0 holds time t0 - RP_LEAD
 
-template <class S, int K, int C, int PD>
+// Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
+// 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 32 output columns.
+//   GEO 0: RP_W = 256, every wave all C rows x 64 columns (C = 32: 1 x 2 blocks, C = 64: 2 x 2)
+//   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
+//   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
+//   instead of 92 KB); the halo costs 1/6 of the columns instead of 1/8.
+template <class S, int K, int C, int PD, int GEO, bool ALLX = false>
 struct PairCfg {
-  static constexpr int TM = C / 32;
-  static constexpr int TN = 2;
+  static constexpr int RP_W = GEO == 0 ? 256 : 192;
+  static constexpr int RP_BN = RP_W - 2 * RP_LEAD;
+  static constexpr int WN = GEO == 0 ? 4 : 2;
+  static constexpr int WM = 4 / WN;
+  static constexpr int TM = C / 32 / WM;
+  static constexpr int TN = RP_W / 32 / WN;
   static constexpr int NC = C / 16;               // 16-channel groups
   static constexpr int HMAX = (K - 1) * 5;        // dilation <= 5
   static constexpr int XROWS = RP_W + HMAX;
   static constexpr int XSZB = XROWS * S::ROWB;    // one X staging buffer (16 channels)
   static constexpr int TROWS = RP_W + 32;         // + zero rows read by the discarded columns
   static constexpr int TSZB = NC * TROWS * S::ROWB;
-  static constexpr int LDSB = (2 * XSZB > TSZB ? 2 * XSZB : TSZB);
+  // ALLX: every 16-channel group of the input window is staged at once (one HBM latency for the
+  // whole of phase 1, no per-chunk barriers); otherwise double-buffered per group
+  static constexpr int XBUFS = ALLX ? NC : 2;
+  static constexpr int LDSB = (XBUFS * XSZB > TSZB ? XBUFS * XSZB : TSZB);
   static constexpr int UPT = (XROWS * 4 + 255) / 256;
-  static_assert((K - 1) / 2 <= RP_LEAD && RP_W - RP_BN == 2 * RP_LEAD, "conv2 halo");
+  static_assert((K - 1) / 2 <= RP_LEAD, "conv2 halo");
+  static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
-template <class S, int K, int C, int PD>
-__global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
-  using P = PairCfg<S, K, C, PD>;
+// C = 32 (16-bit-pair schemes): ask for 3 waves per SIMD (<= 168 VGPRs + AGPRs): the LDS already
+// allows three workgroups per CU, the unconstrained allocation (173) allowed two
+template <class S, int K, int C, int PD, int GEO, bool ALLX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 && S::ROWB <= 80 ? 3 : 1)))
+void resblock_pair_kernel(ResPairArgs pa) {
+  using P = PairCfg<S, K, C, PD, GEO, ALLX>;
+  constexpr int RP_W = P::RP_W, RP_BN = P::RP_BN;
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC;
@@ -51,6 +69,9 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
   const int wave = tid >> 6;
   const int half = lane >> 5;
   const int l32 = lane & 31;
+  const int wm = __builtin_amdgcn_readfirstlane(wave / P::WN);
+  const int wn = wave % P::WN;
+  const int mrow0 = wm * TM * 32;  // first output channel of this wave
   const int t0 = blockIdx.x * RP_BN;
   const int b = blockIdx.z;
   const int d = a1.dil;
@@ -76,15 +97,17 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
     uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
     ulds[i] = r < XW ? r * S::ROWB + 8 * q : -1;
   }
-  f32x4 xreg[P::UPT];
+  f32x4 xall[ALLX ? NC : 1][P::UPT];
   auto load_x = [&](int c) {
+    f32x4 (&xreg)[P::UPT] = xall[ALLX ? c : 0];
     const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * T, (unsigned)(C - c * 16) * chb);
 #pragma unroll
     for (int i = 0; i < P::UPT; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
   };
-  auto store_x = [&](int buf) {
+  auto store_x = [&](int buf, int c) {
+    const f32x4 (&xreg)[P::UPT] = xall[ALLX ? c : 0];
     unsigned char* xl = smem + buf * P::XSZB;
 #pragma unroll
     for (int i = 0; i < P::UPT; ++i) {
@@ -107,7 +130,7 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
 
   rsrc_t ra[TM];
 #pragma unroll
-  for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a1.w + ((size_t)m * NC * K) * (NP * 256), 0xFFFFFFFFu);
+  for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a1.w + ((size_t)(wm * TM + m) * NC * K) * (NP * 256), 0xFFFFFFFFu);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -139,7 +162,7 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
         for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
   };
 
-  const int xrow0 = wave * 64 + l32;
+  const int xrow0 = wn * TN * 32 + l32;
   auto read_x = [&](const unsigned char* xl, int k, f32x4 (*dst)[NP]) {
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
@@ -149,13 +172,20 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
     }
   };
 
-  load_x(0);
-  store_x(0);
+  if constexpr (ALLX) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) load_x(c);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) store_x(c, c);
+  } else {
+    load_x(0);
+    store_x(0, 0);
+  }
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const unsigned char* xl = smem + (c & 1) * P::XSZB;
-    if (c + 1 < NC) load_x(c + 1);
+    const unsigned char* xl = smem + (ALLX ? c : (c & 1)) * P::XSZB;
+    if (!ALLX && c + 1 < NC) load_x(c + 1);
     read_x(xl, 0, bcur);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -174,8 +204,8 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
           for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
       }
     }
-    if (c + 1 < NC) store_x((c + 1) & 1);
-    __syncthreads();
+    if (!ALLX && c + 1 < NC) store_x((c + 1) & 1, c + 1);
+    if (!ALLX || c + 1 == NC) __syncthreads();  // ALLX: only before xt overwrites the window
   }
 
   // ------------------------------------------------------------------ convs1 epilogue -> xt (LDS)
@@ -187,7 +217,7 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
     for (int m = 0; m < TM; ++m) {
       float bv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bv[r] = bload(rb1, (unsigned)(m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+      for (int r = 0; r < 16; ++r) bv[r] = bload(rb1, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
         const int t = tx0 + xrow0 + n * 32;
@@ -225,7 +255,7 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
         const int row = xrow0 + n * 32;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int co = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
           unsigned short h0[NP], h1[NP];
           S::split(acc[m][n][r] * tscale, h0);
           S::split(acc[m][n][r + 1] * tscale, h1);
@@ -245,7 +275,7 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
     // ---------------------------------------------------------------- phase 2: convs2 from LDS
     const Conv1dArgs& a2 = pa.c2;
 #pragma unroll
-    for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a2.w + ((size_t)m * NC * K) * (NP * 256), 0xFFFFFFFFu);
+    for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a2.w + ((size_t)(wm * TM + m) * NC * K) * (NP * 256), 0xFFFFFFFFu);
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -294,21 +324,42 @@ __global__ __launch_bounds__(256) void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
         for (int n = 0; n < TN; ++n) acc[m][n] *= sc2;
     }
-    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wave * 64, 0, lane, t0 + RP_BN);
+    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN);
   }
 }
 
 namespace {
-template <class S, int K, int C>
+// TTS_MI355X_PAIR_ALLX=0 keeps the double-buffered per-group staging (A/B runs)
+bool pair_allx() {
+  static const bool v = [] {
+    const char* e = std::getenv("TTS_MI355X_PAIR_ALLX");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+template <class S, int K, int C, int GEO>
 void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
-  dim3 grid(ceil_div(a.c1.Tout, RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2>), grid, dim3(256), 0, s, a);
+  dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
+  // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32 (scripts/ab_pair_allx.sh)
+  if (C == 64 && pair_allx()) hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, false>), grid, dim3(256), 0, s, a);
+}
+
+// TTS_MI355X_PAIR_GEO64=0 selects the wide (256-column) geometry at 64 channels (A/B runs)
+int pair_geo64() {
+  static const int g = [] {
+    const char* e = std::getenv("TTS_MI355X_PAIR_GEO64");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return g;
 }
 
 template <class S, int K>
 void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
-  if (C == 32) launch_pair_t<S, K, 32>(a, B, s);
-  else if (C == 64) launch_pair_t<S, K, 64>(a, B, s);
+  if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
+  else if (C == 64 && pair_geo64() == 0) launch_pair_t<S, K, 64, 0>(a, B, s);
+  else if (C == 64) launch_pair_t<S, K, 64, 1>(a, B, s);
   else throw Error(3, "resblock pair: channels must be 32 or 64");
 }
 
@@ -327,11 +378,11 @@ bool resblock_pair_supported(int mode, int C, int K, int dil) {
   return is_split_mode(mode) && (C == 32 || C == 64) && (K == 3 || K == 7 || K == 11) && dil >= 1 && dil <= 5;
 }
 
-// Where the fused form is the faster one (MI355X A/B, scripts/ab_fusion.sh, f16x3): every
-// 32-channel iteration (-21..-37%); at 64 channels only k3 (-6%): the k7/k11 iterations are
-// MFMA-heavier and the 141 KB of LDS (xt for 64 channels) leaves one workgroup per CU.
+// Where the fused form is the faster one (MI355X A/B, f16x3): every 32-channel iteration
+// (-21..-37%, scripts/ab_fusion.sh) and, with the 192-column geometry (two workgroups per CU),
+// every 64-channel one (k3 -20%, k7 -11%, k11 -1%; scripts/ab_pair_geo.sh).
 bool resblock_pair_preferred(int mode, int C, int K, int dil) {
-  return resblock_pair_supported(mode, C, K, dil) && (C == 32 || K == 3);
+  return resblock_pair_supported(mode, C, K, dil);
 }
 
 void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s) {
