@@ -67,6 +67,7 @@ struct Conv1dArgs {
   int64_t o_bstride;     // floats between batch items of res / y / z (0 = Cout*Tout)
   int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
   int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
+  int xcd_remap;         // split kernels: XCD-aware tile order (set by launch_conv1d_split)
 };
 
 // One fused ResBlock1 iteration (kernels_resblock.hip): c1 = convs1[m] (x, weights, dilation,

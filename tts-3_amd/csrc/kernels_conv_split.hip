@@ -24,6 +24,7 @@
 // the split.  One step = (16 input channels, one tap): NP*TM A loads, NP*TN LDS reads,
 // NPROD*TM*TN MFMAs.
 #include <algorithm>
+#include <cstdlib>
 
 #include "split_device.hpp"
 
@@ -116,9 +117,17 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, 
   // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
-  if (mode == MATH_FP32_F16X3) launch_split_h3(a, B, K, tile, s);
-  else if (mode == MATH_BF16) launch_split_b1(a, B, K, tile, s);
-  else launch_split_x6(a, B, K, tile, s);
+  // XCD-aware tile order for multi-m-block launches (TTS_MI355X_XCD_REMAP=1 enables it; it measured
+  // neutral: the ConvTranspose weights re-read per XCD are served by the 256 MB Infinity Cache)
+  static const bool remap = [] {
+    const char* e = std::getenv("TTS_MI355X_XCD_REMAP");
+    return e && e[0] == '1';  // measured neutral (MI355X A/B): off by default
+  }();
+  Conv1dArgs ar = a;
+  ar.xcd_remap = remap && ceil_div(a.Cout, conv1d_split_tile(mode, tile).BM) > 1 ? 1 : 0;
+  if (mode == MATH_FP32_F16X3) launch_split_h3(ar, B, K, tile, s);
+  else if (mode == MATH_BF16) launch_split_b1(ar, B, K, tile, s);
+  else launch_split_x6(ar, B, K, tile, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

@@ -39,9 +39,23 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
 
-  const int t0 = blockIdx.x * BN;
-  const int mt = blockIdx.y;
-  const int b = blockIdx.z;
+  // XCD-aware tile order (cdna_hip_programming.md T1, bijective form): blocks that share an XCD
+  // (same linear id mod 8) get one contiguous range of the (time tile, batch, m-block) order with
+  // the m-block slowest, so an XCD's L2 holds the weights of one or two m-blocks instead of all
+  // of them (the 8 / 16 m-block ConvTranspose layers stream 2-8 MB of weights per launch).
+  int bx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
+  if (a.xcd_remap) {
+    const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    const unsigned nwg = gx * gy * gz;
+    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const unsigned xcd = orig & 7u, q = nwg >> 3, r = nwg & 7u;
+    const unsigned wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    bx = (int)(wgid % gx);
+    const unsigned rest = wgid / gx;
+    b = (int)(rest % gz);
+    mt = (int)(rest / gz);
+  }
+  const int t0 = bx * BN;
   const int d = a.dil;
   const int XW = BN + (K - 1) * d;
   const int Tin = a.Tin;
