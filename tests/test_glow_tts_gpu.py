@@ -23,7 +23,7 @@ MEL_MAX_ABS = 1e-4
 MEL_REL_RMS = 2e-5
 
 
-def build_encoder(cfg, seed, device, math_mode="fp32"):
+def build_encoder(cfg, seed, device, math_mode="fp32x6"):
     e = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
                 "rel_pos_transformer", cfg["encoder_params"], mean_only=cfg["mean_only"],
                 use_prenet=cfg["use_prenet"], math_mode=math_mode)
@@ -47,8 +47,9 @@ def build_glow_tts(meta, device, decoder_math_mode="fp32"):
 @pytest.mark.parametrize("name,meta,arr", GENC + [(n, dict(m, config=m["encoder"], seed=m["eseed"]), a)
                                                    for n, m, a in GTTS],
                          ids=[g[0] for g in GENC + GTTS])
-def test_encoder_vs_reference(cuda_device, name, meta, arr):
-    e = build_encoder(meta["config"], meta["seed"], cuda_device)
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+def test_encoder_vs_reference(cuda_device, name, meta, arr, mode):
+    e = build_encoder(meta["config"], meta["seed"], cuda_device, mode)
     tok = torch.from_numpy(arr["tokens"]).to(cuda_device)
     lens = torch.from_numpy(arr["lengths"]).to(cuda_device)
     x_m, x_logs, logw, x_mask = e(tok, lens)
@@ -62,11 +63,13 @@ def test_encoder_vs_reference(cuda_device, name, meta, arr):
 @pytest.mark.parametrize("B,T,lengths,window", [
     (1, 1, [1], None), (2, 9, [9, 4], 4), (3, 70, [70, 65, 1], None), (4, 200, [200, 133, 64, 7], 4),
 ])
-def test_encoder_vs_oracle(cuda_device, B, T, lengths, window):
-    """Shapes around the kernels' tile edges (8-query blocks, 64-key chunks), and T = 1."""
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+def test_encoder_vs_oracle(cuda_device, B, T, lengths, window, mode):
+    """Shapes around the kernels' tile edges (8-query blocks, 64-key chunks, 16-column LayerNorm
+    blocks, 128-column conv tiles), and T = 1."""
     ep = dict(GLOW_TTS_ENCODER["encoder_params"], rel_attn_window_size=window)
     cfg = dict(GLOW_TTS_ENCODER, num_chars=50, encoder_params=ep)
-    e = build_encoder(cfg, 7 + T, cuda_device)
+    e = build_encoder(cfg, 7 + T, cuda_device, mode)
     tok = synthetic.tokens(B, T, 50, seed=T)
     lens = torch.tensor(lengths)
     outs = e(tok.to(cuda_device), lens.to(cuda_device))

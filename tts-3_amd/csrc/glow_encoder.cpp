@@ -92,7 +92,9 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
                       int k) {
     const int Cout = rows_each * (int)parts.size();
     cv.Cin = Cin; cv.Cout = Cout; cv.K = k;
-    cv.tile = conv_tile_for(mode, Cout, k, Cin, 1, false);
+    // text batches are short (a 16 x 128-token batch is 2,048 columns): the split modes take the
+    // 32x128 tile (4 waves side by side) so a conv launches Cout/32 x B workgroups, not Cout/128 x B
+    cv.tile = is_split_mode(mode) ? 16 : conv_tile_for(mode, Cout, k, Cin, 1, false);
     const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
     std::vector<float> w((size_t)Cout * Cin * k), b(Cout);

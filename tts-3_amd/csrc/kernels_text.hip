@@ -47,52 +47,77 @@ void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, floa
 
 // ---------------------------------------------------------------------------------------
 // y = LayerNorm_C(a [+ r]) * gamma + beta, then optional relu, then * mask.
-// One workgroup = 64 time columns x 4 waves; each wave sums a quarter of the channels, the
-// partial sums meet in LDS.  Two-pass mean / variance exactly as the reference formula.
-// y may alias a or r (every element is read by the thread that writes it).
+// One workgroup = 16 time columns x 16 channel slices (a 16-lane group reads 64 contiguous bytes
+// of one channel row); the partial sums meet in LDS.  Two-pass mean / variance exactly as the
+// reference formula.  A 16 x 128-token batch is 128 workgroups (latency-bound: each thread holds
+// at most C/16 values in registers between the passes).  y may alias a or r.
 // ---------------------------------------------------------------------------------------
+constexpr int LN_T = 16;
+constexpr int LN_S = 16;
+constexpr int LN_MAXV = 48;  // C <= 768
+
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* a, const float* r, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, const float* __restrict__ mask,
                                                         float* y, int C, int T, float eps, int relu) {
-  __shared__ float part[4][64];
+  __shared__ float part[LN_S][LN_T];
   const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int t = blockIdx.x * 64 + lane;
+  const int col = threadIdx.x & (LN_T - 1);
+  const int sl = threadIdx.x / LN_T;
+  const int t = blockIdx.x * LN_T + col;
   const bool ok = t < T;
   const size_t base = (size_t)b * C * T + (ok ? t : 0);
-  auto val = [&](int c) {
-    float v = a[base + (size_t)c * T];
-    if (r) v += r[base + (size_t)c * T];
-    return v;
-  };
+  float v[LN_MAXV];
   float s = 0.f;
-  for (int c = w; c < C; c += 4) s += val(c);
-  part[w][lane] = s;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    v[i] = 0.f;
+    if (c < C) {
+      v[i] = a[base + (size_t)c * T];
+      if (r) v[i] += r[base + (size_t)c * T];
+      s += v[i];
+    }
+  }
+  part[sl][col] = s;
   __syncthreads();
-  const float mean = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / (float)C;
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_S; ++i) tot += part[i][col];
+  const float mean = tot / (float)C;
   __syncthreads();
   float q = 0.f;
-  for (int c = w; c < C; c += 4) {
-    const float d = val(c) - mean;
-    q += d * d;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    if (c < C) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
   }
-  part[w][lane] = q;
+  part[sl][col] = q;
   __syncthreads();
-  const float var = (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / (float)C;
+  float qt = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_S; ++i) qt += part[i][col];
+  const float var = qt / (float)C;
   const float rs = 1.f / sqrtf(var + eps);
   const float m = mask ? mask[(size_t)b * T + (ok ? t : 0)] : 1.f;
   if (!ok) return;
-  for (int c = w; c < C; c += 4) {
-    float v = (val(c) - mean) * rs * gamma[c] + beta[c];
-    if (relu) v = fmaxf(v, 0.f);
-    y[base + (size_t)c * T] = v * m;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    if (c < C) {
+      float o = (v[i] - mean) * rs * gamma[c] + beta[c];
+      if (relu) o = fmaxf(o, 0.f);
+      y[base + (size_t)c * T] = o * m;
+    }
   }
 }
 
 void launch_layernorm(const float* a, const float* r, const float* gamma, const float* beta, const float* mask,
                       float* y, int B, int C, int T, float eps, bool relu, hipStream_t s) {
-  dim3 grid(ceil_div(T, 64), B);
+  TTS_REQUIRE(C <= LN_S * LN_MAXV, 3, "LayerNorm: more than 768 channels");
+  dim3 grid(ceil_div(T, LN_T), B);
   hipLaunchKernelGGL(layernorm_kernel, grid, dim3(256), 0, s, a, r, gamma, beta, mask, y, C, T, eps, relu ? 1 : 0);
 }
 

@@ -131,7 +131,7 @@ def _f32(t: torch.Tensor) -> np.ndarray:
 
 class Encoder(nn.Module):
     def __init__(self, num_chars, out_channels, hidden_channels, hidden_channels_dp, encoder_type, encoder_params,
-                 dropout_p_dp=0.1, mean_only=False, use_prenet=True, c_in_channels=0, math_mode: str = "fp32"):
+                 dropout_p_dp=0.1, mean_only=False, use_prenet=True, c_in_channels=0, math_mode: str = "fp32x6"):
         super().__init__()
         if encoder_type.lower() != "rel_pos_transformer":
             raise NotImplementedError(f"encoder_type '{encoder_type}' is not implemented on the MI355X path "
@@ -317,10 +317,11 @@ class GlowTTS(nn.Module):
     ``config`` is a ``GlowTTSConfig``-like object or dict with the reference's field names
     (glow_tts_config.py:103-152); missing fields take the reference defaults.  ``num_chars`` is
     required (the reference takes it from the tokenizer, glow_tts.py:63-66).
-    ``math_mode`` / ``decoder_math_mode`` select the conv arithmetic (encoder fp32 by default:
-    the durations are ceil()-quantised, so the encoder keeps exact fp32 arithmetic)."""
+    ``math_mode`` / ``decoder_math_mode`` select the conv arithmetic.  The encoder's durations are
+    ceil()-quantised, so it runs an fp32-faithful mode: ``"fp32x6"`` by default (bf16x6 split, as
+    accurate as fp32 against the fp64 reference) or ``"fp32"``; the decoder defaults to the same."""
 
-    def __init__(self, config=None, math_mode: str = "fp32", decoder_math_mode: Optional[str] = None, **overrides):
+    def __init__(self, config=None, math_mode: str = "fp32x6", decoder_math_mode: Optional[str] = None, **overrides):
         super().__init__()
         cfg = dict(overrides)
 
