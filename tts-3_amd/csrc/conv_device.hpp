@@ -11,6 +11,9 @@ namespace tts {
 // drops stores whose offset is >= num_records.  OOB_OFF marks a lane's access invalid (callers
 // keep voffset + soffset < 2^32, i.e. every addressed plane < 2 GiB; checked on the host).
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned OOB_OFF = 0x80000000u;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
@@ -153,6 +156,54 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
       const int mm = tbase + n * 32 + l32;
+      if (U == 8) {
+        // registers 4i..4i+3 are phases 4*half .. 4*half+3 of channel co: samples t0 .. t0+3 with
+        // t0 = 8*mm + 4*half - 4 (16-B aligned, wholly inside or outside [0, To)): one dwordx4
+        // store each, and a wave's 64 lanes write 1 KiB of one row contiguously
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rho = cobase + m * 32 + 8 * i + 4 * half;
+          const int co = rho >> 3;
+          const int t0 = (mm << 3) + 4 * half - 4;
+          const unsigned off = (t0 >= 0 && t0 < To) ? ((unsigned)co * (unsigned)To + (unsigned)t0) * 4u : OOB_OFF;
+          f32x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = (acc[m][n][4 * i + j] + bv[4 * i + j]) + cv[4 * i + j];
+            if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v[j]));
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)off, 0, 0);
+        }
+        continue;
+      }
+      if (U == 2) {
+        // registers r, r+1 (r even) are phases 0, 1 of channel co: samples 2*mm - 1, 2*mm, one
+        // dwordx2 store (dword-aligned) unless the pair straddles the plane's start or end
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int rho = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          const int co = rho >> 1;
+          const int t = 2 * mm - 1;
+          const float v0 = (acc[m][n][r] + bv[r]) + cv[r];
+          const float v1 = (acc[m][n][r + 1] + bv[r + 1]) + cv[r + 1];
+          const unsigned rowoff = (unsigned)co * (unsigned)To;
+          if (t >= 0 && t + 1 < To) {
+            if (AMAX && co < Cr) vmax = fmaxf(vmax, fmaxf(fabsf(v0), fabsf(v1)));
+            const f32x2 v = {v0, v1};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rout, (int)((rowoff + (unsigned)t) * 4u), 0, 0);
+          } else {
+            const unsigned off0 = (t >= 0 && t < To) ? (rowoff + (unsigned)t) * 4u : OOB_OFF;
+            const unsigned off1 = (t + 1 >= 0 && t + 1 < To) ? (rowoff + (unsigned)t + 1u) * 4u : OOB_OFF;
+            if (AMAX && co < Cr) {
+              if (off0 != OOB_OFF) vmax = fmaxf(vmax, fabsf(v0));
+              if (off1 != OOB_OFF) vmax = fmaxf(vmax, fabsf(v1));
+            }
+            bstore(rout, v0, off0, 0u);
+            bstore(rout, v1, off1, 0u);
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rho = cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
