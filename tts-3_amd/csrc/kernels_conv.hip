@@ -387,41 +387,84 @@ __global__ __launch_bounds__(256) void convT_mfma_kernel(ConvTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Tail: y = tanh(b + sum_ci sum_k w[ci][k] * lrelu(z[ci][t+k-3], slope)), one output per thread.
+// Tail: y = tanh(b + sum_ci sum_k w[ci][k] * lrelu(z[ci][t+k-3], slope)).
+// One workgroup = 1024 samples, 4 consecutive per thread.  The input window streams through LDS
+// in chunks of 8 channels, double-buffered: the next chunk's loads are in flight while the
+// current one is consumed (the kernel is an HBM read of the Cin-channel plane; one output per
+// thread with the whole window staged first left it latency-bound at 1.5 TB/s).
+// LDS row j <-> time t0 - 4 + j, so the interior lands 16-B aligned at j = 4 + 4*tid.
 // ---------------------------------------------------------------------------------------
-constexpr int POST_T = 256;
+constexpr int POST_T = 1024;
 constexpr int POST_K = 7;
+constexpr int POST_C = 8;
+constexpr int POST_W = POST_T + 8;
+constexpr int POST_MAXC = 64;
 
 __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float psmem[];
+  __shared__ __attribute__((aligned(16))) float zs[2][POST_C][POST_W];
+  __shared__ float ws[POST_MAXC * POST_K];
   const int Cin = a.Cin;
   const int T = a.T;
-  constexpr int XW = POST_T + POST_K - 1;
-  float* zs = psmem;                 // [Cin][XW]
-  float* ws = psmem + Cin * XW;      // [Cin][7]
   const int tid = threadIdx.x;
   const int t0 = blockIdx.x * POST_T;
   const int b = blockIdx.y;
   const float* zb = a.z + (size_t)b * Cin * T;
-  for (int e = tid; e < Cin * XW; e += 256) {
-    const int r = e / XW;
-    const int col = e - r * XW;
-    const int ts = t0 - (POST_K / 2) + col;
-    float v = 0.f;
-    if (ts >= 0 && ts < T) v = lrelu(zb[(size_t)r * T + ts], a.in_slope);
-    zs[e] = v;
-  }
+  const rsrc_t rz = make_rsrc(zb, (unsigned)Cin * (unsigned)T * 4u);
+  const float slope = a.in_slope;
   for (int e = tid; e < Cin * POST_K; e += 256) ws[e] = a.w[e];
-  __syncthreads();
-  const int t = t0 + tid;
-  if (t < T) {
-    float acc = a.bias;
-    for (int ci = 0; ci < Cin; ++ci) {
+  // per thread: 4 interior samples t0 + 4*tid + j, and for tid < 6 one halo sample
+  const int ti = t0 + 4 * tid;
+  const int th = tid < 3 ? t0 - 3 + tid : t0 + POST_T + (tid - 3);  // halo times (tid < 6)
+  const int jh = tid < 3 ? 1 + tid : POST_T + 4 + (tid - 3);
+  const bool hok = tid < 6 && th >= 0 && th < T;
+  const int nch = (Cin + POST_C - 1) / POST_C;
+  float xi[POST_C][4], xh[POST_C];
+  auto load = [&](int ch) {
 #pragma unroll
-      for (int k = 0; k < POST_K; ++k) acc = fmaf(ws[ci * POST_K + k], zs[ci * XW + tid + k], acc);
+    for (int c = 0; c < POST_C; ++c) {
+      const int ci = ch * POST_C + c;
+      const unsigned row = (unsigned)ci * (unsigned)T;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        xi[c][j] = bload(rz, (ci < Cin && ti + j < T) ? (row + (unsigned)(ti + j)) * 4u : OOB_OFF, 0u);
+      xh[c] = bload(rz, (ci < Cin && hok) ? (row + (unsigned)th) * 4u : OOB_OFF, 0u);
     }
-    a.y[(size_t)b * T + t] = tanhf(acc);
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < POST_C; ++c) {
+      f32x4 v = {lrelu(xi[c][0], slope), lrelu(xi[c][1], slope), lrelu(xi[c][2], slope), lrelu(xi[c][3], slope)};
+      *reinterpret_cast<f32x4*>(&zs[buf][c][4 + 4 * tid]) = v;
+      if (tid < 6) zs[buf][c][jh] = lrelu(xh[c], slope);
+    }
+  };
+  float acc[4] = {a.bias, a.bias, a.bias, a.bias};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load(ch + 1);
+#pragma unroll
+    for (int c = 0; c < POST_C; ++c) {
+      const int ci = ch * POST_C + c;
+      if (ci >= Cin) break;
+      // outputs t0 + 4*tid + o use rows 1 + 4*tid + o + k, k < 7: rows 4*tid .. 4*tid + 11
+      const f32x4 r0 = *reinterpret_cast<const f32x4*>(&zs[buf][c][4 * tid]);
+      const f32x4 r1 = *reinterpret_cast<const f32x4*>(&zs[buf][c][4 * tid + 4]);
+      const f32x4 r2 = *reinterpret_cast<const f32x4*>(&zs[buf][c][4 * tid + 8]);
+      const float row[12] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int k = 0; k < POST_K; ++k) acc[o] = fmaf(ws[ci * POST_K + k], row[1 + o + k], acc[o]);
+    }
+    if (ch + 1 < nch) store(buf ^ 1);
+    __syncthreads();
   }
+  const rsrc_t ry = make_rsrc(a.y + (size_t)b * T, (unsigned)T * 4u);
+#pragma unroll
+  for (int o = 0; o < 4; ++o) bstore(ry, tanhf(acc[o]), ti + o < T ? (unsigned)(ti + o) * 4u : OOB_OFF, 0u);
 }
 
 __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const float* Wc, const float* bc,
@@ -586,10 +629,10 @@ void launch_convT(const ConvTArgs& a, int B, int U, int tile, hipStream_t s) {
 }
 
 void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
-  const size_t lds = (size_t)a.Cin * (POST_T + POST_K - 1 + POST_K) * sizeof(float);
-  TTS_REQUIRE(lds <= 64 * 1024, 3, "conv_post: too many input channels");
+  TTS_REQUIRE(a.Cin >= 1 && a.Cin <= POST_MAXC, 3, "conv_post: more than 64 input channels");
+  TTS_REQUIRE((int64_t)a.Cin * a.T * 4 < (int64_t(1) << 31), 3, "conv_post: channel plane exceeds 2 GiB");
   dim3 grid(ceil_div(a.T, POST_T), B);
-  hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), 0, s, a);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
