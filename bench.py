@@ -68,6 +68,7 @@ def parse():
     p.add_argument("--no-glow", action="store_true", help="skip the Glow-TTS decoder measurement")
     p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
     p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
+    p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
     return p.parse_args()
 
@@ -330,6 +331,56 @@ def xtts_decoder_bench(dev, math_mode, steps=10, warmup=3, B=16, T=64):
             "rtf": (ms / 1e3) / (wav.numel() / 24000)}
 
 
+def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
+    """Config 5 per GPU (batch 64 over 8 GPUs = 8 utterances each): VITS waveform path,
+    z_p [B, 192, T] -> ResidualCouplingBlocks reverse (4 flows, speaker-conditioned) -> z * mask ->
+    HiFiGAN decoder (in 192, 512 ch, cond_layer, no conv_post bias, no padding; vits.py:1156-1162)."""
+    from tts_amd import synthetic
+    from tts_amd.config import VITS_DECODER, VITS_FLOW
+    from tts_amd.tts import ResidualCouplingBlocks
+    from tts_amd.vocoder import HifiganGenerator
+
+    fcfg = dict(VITS_FLOW, cond_channels=cond)
+    dcfg = dict(VITS_DECODER, cond_channels=cond)
+    fsd = synthetic.vits_flow_state_dict(**fcfg, seed=2469)
+    dsd = synthetic.hifigan_state_dict(**dcfg, seed=99, weight_norm=False)
+    gen = torch.Generator().manual_seed(9)
+    zp = torch.randn(B, 192, T, generator=gen).to(dev)
+    mask = torch.ones(B, 1, T, device=dev)
+    g = torch.randn(B, cond, 1, generator=gen).to(dev)
+    out = {"workload": f"VITS waveform path, [{B}, 192, {T}] latents (4-flow reverse + 512-ch HiFiGAN decoder, "
+                       f"speaker cond {cond}) per GPU", "variants": {}}
+    for label, (fmode, dmode) in {"bf16": ("bf16", "bf16"), "fp32_faithful": ("fp32x6", "f16x3")}.items():
+        flow = ResidualCouplingBlocks(fcfg["channels"], fcfg["hidden_channels"], fcfg["kernel_size"],
+                                      fcfg["dilation_rate"], fcfg["num_layers"], num_flows=fcfg["num_flows"],
+                                      cond_channels=cond, math_mode=fmode)
+        flow.load_state_dict(fsd)
+        flow = flow.to(dev)
+        dec = HifiganGenerator(**{k: v for k, v in dcfg.items()}, math_mode=dmode)
+        with contextlib.redirect_stdout(sys.stderr):
+            dec.remove_weight_norm()
+        dec.load_state_dict(dsd)
+        dec = dec.to(dev)
+
+        def step():
+            z = flow(zp, mask, g=g, reverse=True)
+            return dec(z * mask, g=g)
+
+        for _ in range(warmup):
+            wav = step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            wav = step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        out["variants"][label] = {"flow_math_mode": fmode, "decoder_math_mode": dmode, "ms_per_step": ms,
+                                  "samples_per_s": wav.numel() / (ms / 1e3),
+                                  "rtf": (ms / 1e3) / (wav.numel() / SAMPLE_RATE)}
+        del flow, dec
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -426,6 +477,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_xtts:
         xtts = xtts_decoder_bench(dev, a.math_mode)
 
+    vits = None
+    if rank == 0 and world == 1 and not a.no_vits:
+        vits = vits_bench(dev)
+
     if rank == 0:
         rec = {
             "metric": METRIC,
@@ -471,6 +526,7 @@ def main():
             "glow_decoder": glow,
             "glow_tts_e2e": e2e,
             "xtts_decoder": xtts,
+            "vits_waveform": vits,
             "accuracy_vs_fp64_oracle": acc,
         }
         if comm:

@@ -9,7 +9,7 @@ tail -1 gpurun_out/ab_pytest.log
 for r in 1 2; do
   for v in $AB; do
     name=${v%%:*}; envs=${v#*:}
-    env ${envs//,/ } timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts > gpurun_out/ab_${name}_$r.json 2>gpurun_out/ab_${name}_$r.err || exit 1
+    env ${envs//,/ } timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits > gpurun_out/ab_${name}_$r.json 2>gpurun_out/ab_${name}_$r.err || exit 1
     python -c "
 import json,re;d=json.load(open('gpurun_out/ab_${name}_$r.json'));b=d['kernel_breakdown_ms']
 print('${name}_$r', round(d['ms_per_step'],2), {k: round(v,2) for k,v in b.items() if re.search('${AB_FILTER:-.}', k)})"
