@@ -81,6 +81,24 @@ bool resblock_pair_supported(int mode, int C, int K, int dil);
 bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster
 void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
 
+// A whole kernel-3 ResBlock1 (three iterations, six convs) in one kernel (kernels_resblock.hip):
+// x stays in registers between iterations (residual), lrelu(x) and xt pass through LDS.
+struct ResBlock3Args {
+  const float* x;           // [B][C][T] block input (the upsampled o)
+  const unsigned* amax_in;  // [B][64] producer statistics of x (f16x3), or nullptr
+  const float* w[6];        // packed conv weights: convs1[0], convs2[0], convs1[1], convs2[1], ...
+  const float* bias[6];
+  int w_exp[6];
+  int dil[3];               // convs1 dilations
+  float* z;                 // MRF accumulator [B][C][T]
+  int zmode;                // 1: z = v, 2: z += v, 3: z = (z + v) / zdiv
+  float zdiv;
+  unsigned* amax_out;       // [B][64] statistics of the stored value, or nullptr
+  int T;
+};
+bool resblock3_supported(int mode, int C, int K, const int* dil);
+void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s);
+
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
 struct ConvTile {
   int BM, BN, TM, TN, CK;

@@ -178,6 +178,18 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
           src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
         }
       }
+      if (cfg_.resblock_type == 1 && rb.fused) {
+        // whole-block fusion (kernels_resblock.hip resblock3_kernel): TTS_MI355X_RESBLOCK3 =
+        // "0" off, "32" 32-channel blocks only, "all" every supported block (default; MI355X A/B
+        // scripts/ab_res3.sh: c32 k3 2.52 -> 1.87 ms, c64 k3 3.18 -> 2.93 ms per batch)
+        static const int policy = [] {
+          const char* e = std::getenv("TTS_MI355X_RESBLOCK3");
+          if (!e) return 1 << 30;
+          if (std::string(e) == "all") return 1 << 30;
+          return std::atoi(e);
+        }();
+        rb.fused3 = ch <= policy && resblock3_supported(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
+      }
       res_.push_back(rb);
     }
   }
@@ -413,7 +425,21 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
       const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
       const int gz = g0 + 1 + cfg_.num_kernels * 6;  // the stage's z / num_kernels
-      if (cfg_.resblock_type == 1 && rb.fused) {
+      if (cfg_.resblock_type == 1 && rb.fused3) {
+        // the three iterations in one launch: o -> MRF z
+        ResBlock3Args ra{};
+        ra.x = bufO; ra.amax_in = slots(g0);
+        for (int c = 0; c < 6; ++c) { ra.w[c] = rb.convs[c].w; ra.bias[c] = rb.convs[c].b; ra.w_exp[c] = rb.convs[c].w_exp; }
+        for (int m = 0; m < 3; ++m) ra.dil[m] = rb.convs[2 * m].dil;
+        ra.z = bufZ; ra.zmode = zlast; ra.zdiv = (float)cfg_.num_kernels;
+        ra.amax_out = j == cfg_.num_kernels - 1 ? slots(gz) : nullptr;
+        ra.T = len;
+        const ConvLayer& L1 = rb.convs[0];
+        const double flops = 12.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
+        const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 6.0 * L1.Cout * L1.Cin * L1.K);
+        const std::string nm = "mrf_block_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
+        run(prof, s, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, s); });
+      } else if (cfg_.resblock_type == 1 && rb.fused) {
         // x_{m+1} = convs2[m](lrelu(convs1[m](lrelu(x_m)))) + x_m in one launch per m; the
         // iterates ping-pong between X and T (o -> X -> T -> X / the MRF z)
         for (int m = 0; m < 3; ++m) {

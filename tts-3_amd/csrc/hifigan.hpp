@@ -93,6 +93,7 @@ class Hifigan {
   struct ResBlock {
     std::vector<ConvLayer> convs;  // type 1: c1_0, c2_0, c1_1, c2_1, c1_2, c2_2; type 2: c_0, c_1
     bool fused = false;            // type 1 iterations run as fused convs1 -> convs2 launches
+    bool fused3 = false;           // type 1, kernel 3: the whole block in one launch (resblock3)
   };
 
   int64_t plane_floats(int B, int T, int pad) const;

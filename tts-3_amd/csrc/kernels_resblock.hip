@@ -398,4 +398,378 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------------------
+// Whole kernel-3 ResBlock1 (hifigan_generator.py:84-99, K = 3, dilations d0..d2) in one kernel:
+//   for m in 0..2:  xt = lrelu(convs1[m](lrelu(x)));  x = convs2[m](xt) + x;   z (+)= x
+// All three iterations run on the same RP_W-column grid (column c <-> time t0 - 16 + c): each conv
+// loses its halo at the grid edges, so the valid columns shrink by d_m + 1 per side per iteration
+// (12 for dilations 1, 3, 5) while the kept ones, [16, RP_W - 16), stay exact.  x lives in the
+// accumulator layout in registers (the residual of every iteration), lrelu(x) and xt alternate
+// in one LDS region as split B operands (X rows: column + 5, xt rows: column + 1).  Columns
+// outside the valid range or outside [0, T) are staged as zeros; in the f16x3 scheme the scale of
+// x1, x2 and of every xt is the workgroup's own power of two over its valid columns (exact and
+// batch-invariant), x0 uses its producer's statistics.  One launch replaces three pair launches:
+// x is read once and z written once instead of five C-planes per iteration.
+// ---------------------------------------------------------------------------------------
+constexpr int R3_XOFF = 5;  // X rows hold column + 5 (convs1 halo up to dilation 5)
+
+template <class S, int C, int GEO>
+struct Res3Cfg {
+  static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_BN = RP_W - 2 * RP_LEAD;
+  static constexpr int WN = GEO == 0 ? 4 : 2;
+  static constexpr int WM = 4 / WN;
+  static constexpr int TM = C / 32 / WM;
+  static constexpr int TN = RP_W / 32 / WN;
+  static constexpr int NC = C / 16;
+  static constexpr int PR = RP_W + 2 * R3_XOFF;  // rows per group (X: RP_W + 10, xt: RP_W + 2)
+  static constexpr int LDSB = NC * PR * S::ROWB;
+  static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
+};
+
+template <class S, int C, int GEO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 || GEO == 2 ? 2 : 1)))
+void resblock3_kernel(ResBlock3Args a) {
+  using P = Res3Cfg<S, C, GEO>;
+  constexpr int K = 3;
+  constexpr int NP = S::NP;
+  constexpr bool H3 = S::SCALED;
+  constexpr int TM = P::TM, TN = P::TN, NC = P::NC, PR = P::PR, RP_W = P::RP_W;
+  constexpr int PD = 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
+  __shared__ float red[4];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int wm = __builtin_amdgcn_readfirstlane(wave / P::WN);
+  const int wn = wave % P::WN;
+  const int mrow0 = wm * TM * 32;
+  const int t0 = blockIdx.x * P::RP_BN;
+  const int b = blockIdx.z;
+  const int T = a.T;
+  const int tx0 = t0 - RP_LEAD;  // time of column 0
+  const int xcol0 = wn * TN * 32 + l32;
+  const unsigned avoff = (unsigned)lane * 16u;
+  const unsigned chb = (unsigned)T * 4u;
+  const float* xb = a.x + (size_t)b * C * T;
+  const rsrc_t rx = make_rsrc(xb, (unsigned)C * chb);
+
+  // ---- prologue: lrelu(x0) pieces for columns [-5, RP_W + 5), one 16-channel group at a time,
+  // and x0 itself in the acc layout
+  int ex = H3 ? amax_exp(a.amax_in, b) : 0;
+  {
+    const float xs = H3 ? ldexpf(1.f, -ex) : 1.f;
+    constexpr int UG = (PR * 4 + 255) / 256;  // units (row, quad) per group per thread
+#pragma unroll 1
+    for (int g = 0; g < NC; ++g) {
+      f32x4 xv[UG];
+#pragma unroll
+      for (int i = 0; i < UG; ++i) {
+        const int u = tid + i * 256;
+        const int q = u & 3;
+        const int r = u >> 2;
+        const int ts = tx0 - R3_XOFF + r;
+        const bool ok = r < PR && ts >= 0 && ts < T;
+        const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < UG; ++i) {
+        const int u = tid + i * 256;
+        const int q = u & 3;
+        const int r = u >> 2;
+        if (r < PR) {
+          u16x4 pv[NP];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned short h[NP];
+            float v = lrelu2(xv[i][j], 0.1f);
+            if (H3) v *= xs;
+            S::split(v, h);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+          }
+#pragma unroll
+          for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(smem + (g * PR + r) * S::ROWB + 8 * q + 32 * p) = pv[p];
+        }
+      }
+    }
+  }
+  f32x16 xr[TM][TN];  // the running residual x (fp32), accumulator layout
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int t = tx0 + xcol0 + n * 32;
+      const bool tok = t >= 0 && t < T;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+      }
+    }
+  __syncthreads();
+
+  f32x16 acc[TM][TN];
+  f32x4 ar[PD + 1][TM][NP], bcur[TN][NP], bnext[TN][NP];
+  rsrc_t ra[TM];
+  // one conv over the LDS region: B rows = column + roff + k * kstep
+  auto conv = [&](int wi, int roff, int kstep) {
+#pragma unroll
+    for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a.w[wi] + ((size_t)(wm * TM + m) * NC * K) * (NP * 256), 0xFFFFFFFFu);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
+    auto read_b = [&](int g, int k, f32x4 (*dst)[NP]) {
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const unsigned char* pp = smem + (g * PR + xcol0 + n * 32 + roff + k * kstep) * S::ROWB + 16 * half;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(pp + 32 * q);
+      }
+    };
+    read_b(0, 0, bcur);
+#pragma unroll
+    for (int g = 0; g < NC; ++g) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int st = g * K + k;
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((st + PD) * NP + q) * 1024u);
+        const bool more = (k + 1 < K) || (g + 1 < NC);
+        if (more) read_b((k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int n = 0; n < TN; ++n)
+              acc[m][n] = S::mfma(ar[0][m][S::PA[e]], bcur[n][S::PB[e]], acc[m][n]);
+#pragma unroll
+        for (int p = 0; p < PD; ++p)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
+        if (more) {
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+        }
+      }
+    }
+  };
+  // block max of |v| over this workgroup (f16x3 scale exponent); every wave must call it
+  auto tile_exp = [&](float vmax) -> int {
+    if (!H3) return 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    if (lane == 0) red[wave] = vmax;
+    __syncthreads();  // also: every wave is done reading the LDS region
+    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    __syncthreads();  // red[] is reused by the next call
+    int e = 0;
+    if (mx > 0.f && mx < INFINITY) {
+      int E;
+      (void)frexpf(mx, &E);
+      e = E - 14;
+    }
+    return e;
+  };
+  // acc-layout values (already zeroed where invalid) -> split pieces at LDS row column + roff;
+  // rows of the region outside [roff, roff + RP_W) are zeroed
+  auto store_pieces = [&](int roff, float scale) {
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int row = xcol0 + n * 32 + roff;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          unsigned short h0[NP], h1[NP];
+          S::split(acc[m][n][r] * scale, h0);
+          S::split(acc[m][n][r + 1] * scale, h1);
+          unsigned char* dst = smem + ((co >> 4) * PR + row) * S::ROWB + 2 * (co & 15);
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            *reinterpret_cast<unsigned*>(dst + 32 * p) = (unsigned)h0[p] | ((unsigned)h1[p] << 16);
+        }
+      }
+    // edge rows: [0, roff) and [roff + RP_W, PR) of every group
+    constexpr int EB = 2 * R3_XOFF * S::ROWB;  // upper bound of edge bytes per group
+    for (int e = tid * 16; e < NC * EB; e += 256 * 16) {
+      const int g = e / EB;
+      const int o = e - g * EB;  // byte in the edge area: first roff rows, then the tail
+      const int lead_b = roff * S::ROWB;
+      const int tail_b = (PR - roff - RP_W) * S::ROWB;
+      if (o < lead_b) *reinterpret_cast<f32x4*>(smem + g * PR * S::ROWB + o) = f32x4{};
+      else if (o - lead_b < tail_b)
+        *reinterpret_cast<f32x4*>(smem + (g * PR + roff + RP_W) * S::ROWB + (o - lead_b)) = f32x4{};
+    }
+  };
+
+  int lo = -R3_XOFF, hi = RP_W + R3_XOFF;  // valid columns of the staged operand
+#pragma unroll 1
+  for (int it = 0; it < 3; ++it) {
+    const int d = a.dil[it];
+    // ---- convs1[it] on lrelu(x) (X rows = column + 5): taps at column + (k - 1) * d
+    conv(2 * it, R3_XOFF - d, d);
+    lo += d;
+    hi -= d;
+    {
+      const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it]) : 1.f;
+      const rsrc_t rb = make_rsrc(a.bias[2 * it], (unsigned)C * 4u);
+      float vmax = 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        float bv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+#pragma unroll
+        for (int n = 0; n < TN; ++n) {
+          const int col = xcol0 + n * 32;
+          const int t = tx0 + col;
+          const bool ok = col >= lo && col < hi && t >= 0 && t < T;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float v = lrelu2(acc[m][n][r] * sc + bv[r], 0.1f);
+            v = ok ? v : 0.f;
+            acc[m][n][r] = v;
+            vmax = fmaxf(vmax, fabsf(v));
+          }
+        }
+      }
+      const int et = tile_exp(vmax);
+      if (!H3) __syncthreads();  // every wave done reading X
+      store_pieces(1, H3 ? ldexpf(1.f, -et) : 1.f);  // xt rows = column + 1
+      __syncthreads();
+      ex = et;
+    }
+    // ---- convs2[it] on xt: taps at column + k - 1 = xt rows column + k
+    conv(2 * it + 1, 0, 1);
+    lo += 1;
+    hi -= 1;
+    const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it + 1]) : 1.f;
+    const rsrc_t rb = make_rsrc(a.bias[2 * it + 1], (unsigned)C * 4u);
+    if (it < 2) {
+      float vmax = 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        float bv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+#pragma unroll
+        for (int n = 0; n < TN; ++n) {
+          const int col = xcol0 + n * 32;
+          const int t = tx0 + col;
+          const bool ok = col >= lo && col < hi && t >= 0 && t < T;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float x1 = (acc[m][n][r] * sc + bv[r]) + xr[m][n][r];  // x = convs2(xt) + x
+            xr[m][n][r] = x1;
+            const float v = ok ? lrelu2(x1, 0.1f) : 0.f;  // the next convs1's operand
+            acc[m][n][r] = v;
+            vmax = fmaxf(vmax, fabsf(v));
+          }
+        }
+      }
+      const int e2 = tile_exp(vmax);
+      if (!H3) __syncthreads();  // every wave done reading xt
+      store_pieces(R3_XOFF, H3 ? ldexpf(1.f, -e2) : 1.f);
+      __syncthreads();
+      ex = e2;
+    } else {
+      // ---- final: x3 = convs2[2](xt) + x2 -> MRF z (kept columns [16, 16 + RP_BN) only)
+      const rsrc_t rz = make_rsrc(a.z + (size_t)b * C * T, (unsigned)C * chb);
+      float vmax = 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        float bv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+#pragma unroll
+        for (int n = 0; n < TN; ++n) {
+          const int col = xcol0 + n * 32;
+          const int t = tx0 + col;
+          const bool keep = col >= RP_LEAD && col < RP_LEAD + P::RP_BN && t >= 0 && t < T;
+          unsigned vo[16];
+          float zv[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            vo[r] = keep ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF;
+            zv[r] = a.zmode >= 2 ? bload(rz, vo[r], 0u) : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float v = (acc[m][n][r] * sc + bv[r]) + xr[m][n][r];
+            if (a.zmode == 2) v = zv[r] + v;
+            else if (a.zmode == 3) v = (zv[r] + v) / a.zdiv;
+            if (keep) vmax = fmaxf(vmax, fabsf(v));
+            bstore(rz, v, vo[r], 0u);
+          }
+        }
+      }
+      if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+    }
+  }
+}
+
+namespace {
+template <class S, int C, int GEO>
+void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
+  dim3 grid(ceil_div(a.T, Res3Cfg<S, C, GEO>::RP_BN), 1, B);
+  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO>), grid, dim3(256), 0, s, a);
+}
+template <class S>
+void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
+  // C = 64: 128 columns (2 waves/SIMD, a quarter of the columns are halo) unless
+  // TTS_MI355X_RES3_GEO64=1 (192 columns, one wave per SIMD)
+  static const int geo64 = [] {
+    const char* e = std::getenv("TTS_MI355X_RES3_GEO64");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  if (C == 32) launch_res3_t<S, 32, 0>(a, B, s);
+  else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
+  else launch_res3_t<S, 64, 2>(a, B, s);
+}
+}  // namespace
+
+bool resblock3_supported(int mode, int C, int K, const int* dil) {
+  if (!is_split_mode(mode) || !(C == 32 || C == 64) || K != 3) return false;
+  int halo = 0;
+  for (int m = 0; m < 3; ++m) {
+    if (dil[m] < 1 || dil[m] > R3_XOFF) return false;
+    halo += dil[m] + 1;
+  }
+  // kept columns [16, RP_W - 16) must stay inside the valid range [-5 + halo, RP_W + 5 - halo)
+  return halo - R3_XOFF <= RP_LEAD;
+}
+
+void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s) {
+  TTS_REQUIRE(resblock3_supported(mode, C, 3, a.dil), 3, "resblock3: unsupported configuration");
+  TTS_REQUIRE(a.zmode >= 1 && a.zmode <= 3 && a.z && a.x && a.x != a.z, 1, "resblock3: bad arguments");
+  TTS_REQUIRE((int64_t)C * a.T * 4 < (int64_t(1) << 31), 3, "resblock3: plane exceeds 2 GiB");
+  if (mode == MATH_FP32_F16X3) launch_res3_s<SchemeH3>(a, B, C, s);
+  else if (mode == MATH_BF16) launch_res3_s<SchemeB1>(a, B, C, s);
+  else launch_res3_s<SchemeX6>(a, B, C, s);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts
