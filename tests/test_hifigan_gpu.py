@@ -113,7 +113,7 @@ def test_op_conv_transpose1d(cuda_device, case, mode):
     assert_close_fp32(y.cpu(), ref, f"convT {case}", **tol(mode))
 
 
-@pytest.mark.parametrize("B,Cin,T", [(2, 32, 1000), (1, 32, 1), (3, 8, 513)])
+@pytest.mark.parametrize("B,Cin,T", [(2, 32, 1000), (1, 32, 1), (3, 8, 513), (2, 64, 3001), (1, 20, 1024)])
 def test_op_conv_post(cuda_device, B, Cin, T):
     g = _rng(T)
     z = torch.randn(B, Cin, T, generator=g)
@@ -172,13 +172,16 @@ def test_generator_stage_parity(cuda_device):
     assert_close_fp32(y.cpu(), arr["stage_conv_pre"], "conv_pre stage", max_abs_tol=1e-5)
 
 
-def test_generator_edge_lengths_vs_oracle(cuda_device):
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3"])
+def test_generator_edge_lengths_vs_oracle(cuda_device, mode):
+    """Lengths around the tile edges of every kernel family, incl. the fused resblock kernels of the
+    split modes (224 / 96-column tiles at C=32 / C=64) and the streaming conv_post (1024 samples)."""
     sd = synthetic.hifigan_state_dict(seed=31, weight_norm=False)
-    g = HifiganGenerator(**V1)
+    g = HifiganGenerator(**V1, math_mode=mode)
     g.remove_weight_norm()
     g.load_state_dict(sd)
     g = g.to(cuda_device)
-    for B, T, pad in [(1, 1, 0), (2, 3, 0), (1, 2, 5), (3, 67, 5)]:
+    for B, T, pad in [(1, 1, 0), (2, 3, 0), (1, 2, 5), (3, 67, 5), (2, 101, 0)]:
         mel = synthetic.mel(B, T, seed=T)
         out = g._run(mel.to(cuda_device), pad, None)
         ref = hifigan_ref.hifigan_forward(sd, mel, pad=pad, dtype=torch.float64, **V1)
