@@ -277,6 +277,7 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "glow_tts":
         return main_glow_tts()
     if len(sys.argv) > 1 and sys.argv[1] == "handoff":
+        main_handoff_range()
         return main_handoff()
     if len(sys.argv) > 1 and sys.argv[1] == "xtts":
         return main_xtts()
@@ -386,6 +387,70 @@ def main_xtts():
                         z_ref_fp64=z64.numpy(), out_ref_fp32=o32.numpy(), out_ref_fp64=o64.numpy())
     print(f"wrote {path}: z {tuple(z32.shape)} out {tuple(o32.shape)} std {o32.std():.4f} "
           f"max|fp32-fp64| {np.abs(o32.numpy() - o64.numpy()).max():.2e}")
+
+
+def reference_functions(path, names, extra_globals):
+    """The named top-level functions / methods of a reference source file, compiled from that file.
+
+    processor.py and numpy_transforms.py import librosa / soundfile at module level (absent here),
+    so the modules cannot be imported; their normalize / denormalize / save_wav bodies need only
+    numpy and scipy, so those function definitions are taken from the reference file with ast and
+    executed as they are (nothing of their text is copied into this repository)."""
+    import ast
+
+    tree = ast.parse(open(path).read())
+    out = {}
+    for node in ast.walk(tree):
+        if isinstance(node, ast.FunctionDef) and node.name in names and node.name not in out:
+            mod = ast.Module(body=[node], type_ignores=[])
+            ns = dict(extra_globals)
+            exec(compile(mod, path, "exec"), ns)  # noqa: S102  (reference code, goldens only)
+            out[node.name] = ns[node.name]
+    return out
+
+
+def main_handoff_range():
+    """G10: AudioProcessor.normalize / denormalize (range normalisation, processor.py:259-336) and
+    numpy_transforms.save_wav's int16 scaling (:430-447), executed from the reference source."""
+    import tempfile
+    import scipy.io.wavfile
+    from types import SimpleNamespace
+
+    proc = os.path.join(REF, "TTS/utils/audio/processor.py")
+    fns = reference_functions(proc, {"normalize", "denormalize"}, {"np": np})
+    nt = reference_functions(os.path.join(REF, "TTS/utils/audio/numpy_transforms.py"), {"save_wav"},
+                             {"np": np, "scipy": scipy, "BytesIO": None})
+    configs = [
+        dict(signal_norm=True, symmetric_norm=True, clip_norm=True, max_norm=4.0, min_level_db=-100, ref_level_db=20),
+        dict(signal_norm=True, symmetric_norm=False, clip_norm=True, max_norm=1.0, min_level_db=-100, ref_level_db=0),
+        dict(signal_norm=True, symmetric_norm=True, clip_norm=False, max_norm=4.0, min_level_db=-100, ref_level_db=20),
+        dict(signal_norm=True, symmetric_norm=False, clip_norm=False, max_norm=2.5, min_level_db=-90, ref_level_db=16),
+    ]
+    rng = np.random.default_rng(12)
+    mel = (rng.standard_normal((45, 80)) * 3).astype(np.float32)  # model_outputs[0]: [T, C]
+    arrays = dict(mel=mel)
+    pairs = []
+    for i, a in enumerate(configs):
+        for j, v in enumerate(configs):
+            ap_t = SimpleNamespace(**a)
+            ap_v = SimpleNamespace(**v)
+            den = fns["denormalize"](ap_t, mel.T).T   # synthesizer.py:414
+            voc = fns["normalize"](ap_v, den.T)       # :416
+            arrays[f"out_{i}_{j}"] = np.asarray(voc)
+            pairs.append([i, j])
+    wavs = [np.tanh(rng.standard_normal(20011)).astype(np.float32) * s_ for s_ in (1.0, 0.3, 0.004)]
+    wavs.append(np.zeros(513, np.float32))
+    for k, w in enumerate(wavs):
+        with tempfile.TemporaryDirectory() as d:
+            fpath = os.path.join(d, "x.wav")
+            nt["save_wav"](wav=w, path=fpath, sample_rate=22050)
+            _, pcm = scipy.io.wavfile.read(fpath)
+        arrays[f"wav_{k}"] = w
+        arrays[f"pcm_{k}"] = pcm
+    meta = dict(kind="handoff_range", configs=configs, pairs=pairs, n_wavs=len(wavs))
+    path = os.path.join(HERE, "handoff_range_t45.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: {len(pairs)} config pairs, {len(wavs)} wavs; pcm dtype {arrays['pcm_0'].dtype}")
 
 
 def main_handoff():

@@ -71,3 +71,20 @@ def test_wav_int16_matches_save_wav_scaling(cuda_device):
         L = int(lens[b])
         assert np.array_equal(out[b, :L], handoff_ref.wav_int16(w[b, 0, :L]))
         assert not out[b, L:].any()
+
+
+HRANGE = goldens("handoff_range")
+
+
+@pytest.mark.parametrize("name,meta,arr", HRANGE, ids=[g[0] for g in HRANGE])
+def test_handoff_and_int16_vs_reference_functions(cuda_device, name, meta, arr):
+    """Bit-exact against the reference's own AudioProcessor.normalize/denormalize and
+    numpy_transforms.save_wav output (tests/golden/make_goldens.py handoff)."""
+    cfgs = meta["configs"]
+    x = torch.from_numpy(arr["mel"][None]).to(cuda_device)  # [1, T, C]
+    for i, j in meta["pairs"]:
+        out = mel_handoff(x, _norm(dict(cfgs[i], sample_rate=22050)), _norm(dict(cfgs[j], sample_rate=22050)))
+        assert np.array_equal(out[0].cpu().numpy(), arr[f"out_{i}_{j}"]), (i, j)
+    for k in range(meta["n_wavs"]):
+        w = torch.from_numpy(arr[f"wav_{k}"][None]).to(cuda_device)
+        assert np.array_equal(wav_to_int16(w)[0].cpu().numpy(), arr[f"pcm_{k}"]), k

@@ -198,3 +198,20 @@ def test_xtts_decoder_oracle_matches_reference(name, meta, arr):
     out = hifigan_ref.hifigan_forward(sd, z, pad=0, g=torch.from_numpy(arr["g"]), dtype=torch.float64,
                                       fold_dtype=torch.float64, **cfg)
     assert max_abs(out.numpy(), arr["out_ref_fp64"]) < 1e-10
+
+
+HRANGE = goldens("handoff_range")
+
+
+@pytest.mark.parametrize("name,meta,arr", HRANGE, ids=[g[0] for g in HRANGE])
+def test_handoff_range_oracle_matches_reference(name, meta, arr):
+    """normalize / denormalize / save_wav scaling executed from the reference source (golden)."""
+    from oracle import handoff_ref
+
+    cfgs = meta["configs"]
+    for i, j in meta["pairs"]:
+        den = handoff_ref.denormalize(arr["mel"].T, cfgs[i]).T
+        out = handoff_ref.normalize(den.T, cfgs[j])
+        assert out.dtype == np.float32 and np.array_equal(out, arr[f"out_{i}_{j}"]), (i, j)
+    for k in range(meta["n_wavs"]):
+        assert np.array_equal(handoff_ref.wav_int16(arr[f"wav_{k}"]), arr[f"pcm_{k}"]), k
