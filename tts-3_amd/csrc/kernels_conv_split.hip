@@ -100,7 +100,12 @@ int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res)
   (void)res;
   if ((K - 1) * dil > (K - 1) * 5) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
   if (mode == MATH_FP32_F16X3) {
-    if (Cout > 64) return 13;
+    // TTS_MI355X_TILE_BIG=<idx> overrides the tile of the Cout > 64 layers (A/B runs)
+    static const int big = [] {
+      const char* e = std::getenv("TTS_MI355X_TILE_BIG");
+      return e ? std::atoi(e) : 13;
+    }();
+    if (Cout > 64) return (big >= 0 && big < kNumSplitTiles) ? big : 13;
     if (Cout > 32) return 10;
     return 14;  // one 16-channel group, 42 KB of LDS: 3 workgroups per CU
   }
