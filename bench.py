@@ -350,7 +350,7 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
     g = torch.randn(B, cond, 1, generator=gen).to(dev)
     out = {"workload": f"VITS waveform path, [{B}, 192, {T}] latents (4-flow reverse + 512-ch HiFiGAN decoder, "
                        f"speaker cond {cond}) per GPU", "variants": {}}
-    for label, (fmode, dmode) in {"bf16": ("bf16", "bf16"), "fp32_faithful": ("fp32x6", "f16x3")}.items():
+    for label, (fmode, dmode) in {"bf16": ("bf16", "bf16"), "fp32_faithful": ("f16x3", "f16x3")}.items():
         flow = ResidualCouplingBlocks(fcfg["channels"], fcfg["hidden_channels"], fcfg["kernel_size"],
                                       fcfg["dilation_rate"], fcfg["num_layers"], num_flows=fcfg["num_flows"],
                                       cond_channels=cond, math_mode=fmode)
@@ -465,13 +465,11 @@ def main():
 
     glow = None
     if rank == 0 and not a.no_glow:
-        # the Glow decoder implements fp32 and fp32x6 (TTS_MATH_FP32_F16X3 is HiFiGAN-only)
-        glow_mode = "fp32x6" if a.math_mode == "f16x3" else a.math_mode  # bf16 runs as is
-        glow = glow_bench(dev, glow_mode, cpu=(world == 1 and not a.no_cpu_baseline))
+        glow = glow_bench(dev, a.math_mode, cpu=(world == 1 and not a.no_cpu_baseline))
 
     e2e = None
     if rank == 0 and world == 1 and not a.no_e2e:
-        e2e = glow_tts_e2e_bench(dev, {"fp32_faithful": ("fp32x6", "f16x3"), "bf16": ("bf16", "bf16")})
+        e2e = glow_tts_e2e_bench(dev, {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")})
 
     xtts = None
     if rank == 0 and world == 1 and not a.no_xtts:

@@ -64,7 +64,8 @@ extern "C" {
  *                     ceiling).  The
  *                     scales come from max-abs statistics each producing kernel records; the
  *                     HiFiGAN executor runs conv_pre (user input, no statistics) in FP32_X6.
- *                     HiFiGAN only: the Glow decoder rejects it (TTS_ERR_UNSUPPORTED).
+ *                     HiFiGAN, the Glow decoder and the VITS flow; the Glow encoder rejects it
+ *                     (TTS_ERR_UNSUPPORTED).
  *   TTS_MATH_BF16     bf16 operands on v_mfma_f32_32x32x16_bf16 with fp32 accumulation and fp32
  *                     activations in HBM (the bf16 arithmetic of configs 3 / 5; not fp32-faithful:
  *                     ~2^-9 relative per product). */
@@ -174,7 +175,7 @@ typedef struct TtsGlowDecoderCfg {
   int num_squeeze;         /* 2 */
   int sigmoid_scale;       /* 0 */
   int c_in_channels;       /* 0 (speaker conditioning not implemented: must be 0) */
-  int math_mode;           /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
+  int math_mode;           /* TTS_MATH_FP32 (default), _X6, _F16X3 or TTS_MATH_BF16 */
 } TtsGlowDecoderCfg;
 
 /* Host weight order, per flow block b < num_flow_blocks (flows 3b, 3b+1, 3b+2):
@@ -319,7 +320,7 @@ typedef struct TtsVitsFlowCfg {
   int num_layers;      /* 4 (num_layers_flow) */
   int num_flows;       /* 4 */
   int cond_channels;   /* speaker embedding size, 0 = none (embedded_speaker_dim) */
-  int math_mode;       /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
+  int math_mode;       /* TTS_MATH_FP32 (default), _X6, _F16X3 or TTS_MATH_BF16 */
 } TtsVitsFlowCfg;
 
 /* Host weight order, per flow f < num_flows (weight norm folded: w = g * v / ||v||):

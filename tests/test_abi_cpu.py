@@ -164,8 +164,9 @@ def test_glow_config_validation():
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, N.MATH_MODES["f16x3"])
-    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
-    assert b"F16X3" in N.lib().tts_last_error()
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 23  # f16x3 accepted (23 tensors per flow)
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, 9)
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
 
 
 def test_math_modes_and_tile_tables():

@@ -25,7 +25,7 @@ def build(cfg, seed, device, math_mode="fp32"):
     return d.to(device)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3", "bf16"])
 @pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
 def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
     d = build(meta["config"], meta["seed"], cuda_device, mode)
@@ -39,11 +39,12 @@ def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
         assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, GLOW_MAX_ABS, GLOW_REL_RMS)
 
 
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
 @pytest.mark.parametrize("B,T,lengths", [(1, 2, [2]), (2, 7, [7, 3]), (4, 400, [400, 399, 200, 1])])
-def test_glow_reverse_vs_oracle(cuda_device, B, T, lengths):
+def test_glow_reverse_vs_oracle(cuda_device, B, T, lengths, mode):
     cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
                num_coupling_layers=4, num_splits=4, num_squeeze=2)
-    d = build(cfg, 99, cuda_device)
+    d = build(cfg, 99, cuda_device, mode)
     g = torch.Generator().manual_seed(T)
     x = torch.randn(B, 80, T, generator=g)
     m = (torch.arange(T)[None] < torch.tensor(lengths)[:, None]).float().unsqueeze(1)
@@ -52,10 +53,11 @@ def test_glow_reverse_vs_oracle(cuda_device, B, T, lengths):
     assert_close_fp32(y.cpu(), ref, f"glow B={B} T={T}", GLOW_MAX_ABS, GLOW_REL_RMS)
 
 
-def test_glow_batch_invariance(cuda_device):
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
+def test_glow_batch_invariance(cuda_device, mode):
     cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
                num_coupling_layers=4, num_splits=4, num_squeeze=2)
-    d = build(cfg, 5, cuda_device)
+    d = build(cfg, 5, cuda_device, mode)
     x = torch.randn(16, 80, 768, generator=torch.Generator().manual_seed(1)).to(cuda_device)
     m = torch.ones(16, 1, 768, device=cuda_device)
     y, _ = d(x, m, reverse=True)

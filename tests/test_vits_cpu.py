@@ -45,8 +45,10 @@ def test_validation_status_codes():
     assert b"even" in lib.tts_last_error()
     c = N.TtsVitsFlowCfg(192, 192, 9, 1, 4, 4, 0, 0)
     assert lib.tts_vits_flow_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
-    c = N.TtsVitsFlowCfg(192, 192, 5, 1, 4, 4, 0, N.MATH_MODES["f16x3"])
-    assert lib.tts_vits_flow_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c = N.TtsVitsFlowCfg(192, 192, 5, 1, 4, 4, 0, N.MATH_MODES["f16x3"])  # f16x3: statistics per conv input
+    assert lib.tts_vits_flow_num_weights(ctypes.byref(c)) > 0
+    c = N.TtsVitsFlowCfg(192, 192, 5, 1, 4, 4, 0, 7)
+    assert lib.tts_vits_flow_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
     assert lib.tts_vits_flow_create(None, None, 0, None) == N.TTS_ERR_INVALID
     assert lib.tts_vits_flow_destroy(None) == N.TTS_OK
 

@@ -16,7 +16,7 @@ from tts_amd.vocoder import HifiganGenerator
 pytestmark = pytest.mark.gpu
 
 VITS = goldens("vits_flow")
-MODES = ["fp32", "fp32x6", "bf16"]
+MODES = ["fp32", "fp32x6", "f16x3", "bf16"]
 
 
 def build(cfg, seed, device, math_mode="fp32"):
@@ -71,7 +71,7 @@ def test_vits_waveform_path(cuda_device, mode):
     """z = flow(z_p, mask, g, reverse); wav = decoder((z * mask), g)  (vits.py:1156-1162)."""
     cond = 8
     fcfg = dict(VITS_FLOW, cond_channels=cond)
-    flow, fsd = build(fcfg, 2469, cuda_device, "fp32" if mode == "f16x3" else mode)
+    flow, fsd = build(fcfg, 2469, cuda_device, mode)
     dcfg = dict(VITS_DECODER, upsample_initial_channel=128, cond_channels=cond)
     dsd = synthetic.hifigan_state_dict(**dcfg, seed=99, weight_norm=False)
     dec = HifiganGenerator(**dcfg, math_mode=mode)

@@ -154,7 +154,8 @@ int conv1d_split_num_tiles(int mode);
 int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res);
 void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
 // slots[b][0..63] = max |x[b]| over n floats per item (fp32 bits, atomicMax; zero them first)
-void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s);
+// stride: floats between batch items (0 = n, contiguous items)
+void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s, int64_t stride = 0);
 
 // Mode-dispatching helpers used by the executors and the op entry points.
 inline bool is_split_mode(int mode) { return mode == MATH_FP32_X6 || mode == MATH_FP32_F16X3 || mode == MATH_BF16; }

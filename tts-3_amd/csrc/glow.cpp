@@ -51,8 +51,6 @@ void glow_validate(const TtsGlowDecoderCfg& c) {
   }
   TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned Glow decoder (c_in_channels > 0) not implemented");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
-  TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3,
-              "Glow decoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
 GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, int device)
@@ -86,7 +84,7 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
     const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);
     const size_t off = host.size();
     host.resize(off + align(n), 0.f);
-    pack_conv(mode, w, Cout, Cin, K, t, host.data() + off);
+    cv.w_exp = pack_conv(mode, w, Cout, Cin, K, t, host.data() + off);
     fix.push_back({off, &cv.w});
     const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
     const size_t offb = host.size();
@@ -123,12 +121,20 @@ GlowDecoder::~GlowDecoder() {
   if (ws_) (void)hipFree(ws_);
 }
 
+// f16x3 statistics: per flow (in execution order) 2L + 2 groups of [B][64] slots: the start conv's
+// input x0, h before each in_layer, acts before each res_skip layer, and the final skip
+size_t GlowDecoder::amax_floats(int B) const {
+  if (cfg_.math_mode != MATH_FP32_F16X3) return 0;
+  return (size_t)cfg_.num_flow_blocks * (2 * cfg_.num_coupling_layers + 2) * B * 64;
+}
+
 void GlowDecoder::reserve(int B, int Th) {
   const int C2 = cfg_.in_channels * cfg_.num_squeeze;
   const int H = cfg_.hidden_channels;
   const size_t plane = (size_t)B * Th;
-  // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1
-  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 8 * sizeof(float);
+  // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1; f16x3: max-abs slot groups
+  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 8 * sizeof(float) +
+                      amax_floats(B) * sizeof(float);
   if (need <= ws_bytes_) return;
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
@@ -158,7 +164,13 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   float* rs = p; p += al(plane * 2 * H);
   float* skip = p; p += al(plane * H);
   float* out = p; p += al(plane * C2);
-  float* msq = p;
+  float* msq = p; p += al(plane);
+  const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(p) : nullptr;
+  const int ng = 2 * L + 2;
+  // slot group: flow fi (execution order), kind 0 = x0, 1 + l = h_l, 1 + L + l = acts_l, 2L + 1 = skip
+  auto slots = [&](int fi, int kind) -> unsigned* { return h3 ? amax + ((size_t)fi * ng + kind) * B * 64 : nullptr; };
+  if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, amax_floats(B) * sizeof(unsigned), s));
 
   // squeeze (decoder.py:128, :8-28); without squeeze the mask is used as is
   const double P = (double)B * Th;  // squeezed positions
@@ -170,9 +182,11 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
     TTS_HIP_CHECK(hipMemcpyAsync(msq, mask, plane * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
 
-  auto conv = [&](const char* name, const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m) {
+  auto conv = [&](const char* name, const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m,
+                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
     Conv1dArgs a{};
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride;
+    a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = cv.w_exp;
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th;
     a.dil = cv.dil; a.pad = cv.dil * (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;
     a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = 0; a.zdiv = 1.f;
@@ -183,16 +197,23 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1
   for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
     const Flow& F = flows_[f];
+    const int fi = cfg_.num_flow_blocks - 1 - f;
+    if (h3)  // statistics of x_0 (the start conv's input), strided over the squeezed channels
+      run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
+          [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
-    conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq);
+    conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq, slots(fi, 0), slots(fi, 1));
     for (int l = 0; l < L; ++l) {
-      conv("glow_wn_in", F.in_layers[l], hb, 0, xin, nullptr);                   // wavenet.py:101
-      run(prof, s, "glow_gate", 0.0, 12.0 * P * H, [&] { launch_glow_gate(xin, acts, B, H, Th, s); });  // :108
-      conv("glow_wn_res_skip", F.res_skip[l], acts, 0, rs, nullptr);             // :109
-      run(prof, s, "glow_wn_update", 0.0, 24.0 * P * H,
-          [&] { launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s); });  // :110-115
+      conv("glow_wn_in", F.in_layers[l], hb, 0, xin, nullptr, slots(fi, 1 + l));  // wavenet.py:101
+      run(prof, s, "glow_gate", 0.0, 12.0 * P * H,
+          [&] { launch_glow_gate(xin, acts, B, H, Th, s, slots(fi, 1 + L + l)); });  // :108
+      conv("glow_wn_res_skip", F.res_skip[l], acts, 0, rs, nullptr, slots(fi, 1 + L + l));  // :109
+      run(prof, s, "glow_wn_update", 0.0, 24.0 * P * H, [&] {
+        launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s,
+                              l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
+      });  // :110-115
     }
-    conv("glow_end", F.end, skip, 0, out, nullptr);                             // glow.py:214
+    conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));        // glow.py:214
     GlowTailArgs ta{};
     ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
     ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;

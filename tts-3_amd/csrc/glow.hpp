@@ -29,9 +29,11 @@ void launch_glow_squeeze(const float* x, const float* mask, float* xs, float* ms
                          int nsq, hipStream_t s);
 void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, int C, int Th, int nsq,
                            hipStream_t s);
-void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s);
+// amax: [B][64] max-abs slots of the output (f16x3 statistics of the next conv's input), or nullptr
+void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s,
+                      unsigned* amax = nullptr);
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,
-                           int Th, int first, int last, hipStream_t s);
+                           int Th, int first, int last, hipStream_t s, unsigned* amax = nullptr);
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s);
 void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStream_t s);  // torch.flip(x, [1])
 
@@ -47,7 +49,7 @@ class GlowDecoder {
 
  private:
   struct Conv {
-    int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0;
+    int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0, w_exp = 0;
     float* w = nullptr;
     float* b = nullptr;
   };
@@ -59,6 +61,7 @@ class GlowDecoder {
     std::vector<Conv> in_layers, res_skip;
   };
   void reserve(int B, int Th);
+  size_t amax_floats(int B) const;
 
   TtsGlowDecoderCfg cfg_;
   int device_;

@@ -32,17 +32,19 @@ namespace tts {
 
 // slots[b][blockIdx.x & 63] = max |x[b]| (grid-stride per item), for inputs without producer
 // statistics
-__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, int64_t n, unsigned* slots) {
-  const float* xb = x + (size_t)blockIdx.z * n;
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, int64_t n, int64_t stride,
+                                                   unsigned* slots) {
+  const float* xb = x + (size_t)blockIdx.z * stride;
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     m = fmaxf(m, fabsf(xb[i]));
   publish_amax(slots, blockIdx.z, m);
 }
 
-void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s) {
+void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s, int64_t stride) {
   const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, (n + 255) / 256));
-  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks, 1, B), dim3(256), 0, s, x, n, slots);
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks, 1, B), dim3(256), 0, s, x, n, stride > 0 ? stride : n,
+                     slots);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
@@ -73,6 +75,8 @@ constexpr ConvTile kSplitTiles[] = {
     {64, 128, 2, 1, 16, 1},   // 17
     {64, 128, 2, 1, 16, 2},   // 18
     {32, 512, 1, 4, 16, 2},   // 19
+    {128, 128, 1, 4, 32, 2},  // 20 waves stacked along Cout: each wave streams its own 32 weight
+    {128, 128, 1, 4, 16, 2},  // 21 rows (half the A fragments of the 2 x 2 layout), 4 B blocks
 };
 constexpr int kNumSplitTiles = sizeof(kSplitTiles) / sizeof(kSplitTiles[0]);
 

@@ -6,6 +6,7 @@
 //                            (InvConvNear inverse) -> normalization.py:96-98 (ActNorm inverse),
 //                            fused: one thread owns the S channels InvConvNear mixes.
 #include "glow.hpp"
+#include "conv_device.hpp"
 
 namespace tts {
 
@@ -40,37 +41,48 @@ __global__ __launch_bounds__(256) void glow_unsqueeze_kernel(const float* xs, co
 }
 
 // acts[b][c][t] = tanh(xin[b][c][t]) * sigmoid(xin[b][c+H][t])
-__global__ __launch_bounds__(256) void glow_gate_kernel(const float* xin, float* acts, int H, int Th) {
+// amax_* ([B][64] slots, or nullptr): max |output| per utterance for the f16x3 consumers
+__global__ __launch_bounds__(256) void glow_gate_kernel(const float* xin, float* acts, int H, int Th,
+                                                        unsigned* amax) {
   const int b = blockIdx.y;
   const int64_t n = (int64_t)H * Th;
+  float vm = 0.f;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float a = xin[(size_t)b * 2 * n + i];
     const float g = xin[(size_t)b * 2 * n + n + i];
     const float sg = 1.f / (1.f + expf(-g));
-    acts[(size_t)b * n + i] = tanhf(a) * sg;
+    const float v = tanhf(a) * sg;
+    acts[(size_t)b * n + i] = v;
+    vm = fmaxf(vm, fabsf(v));
   }
+  if (amax) publish_amax(amax, b, vm);
 }
 
 // not last: h = (h + rs[:H]) * mask ; skip (+)= rs[H:]       last: skip = (skip + rs) * mask
 __global__ __launch_bounds__(256) void glow_wn_update_kernel(float* h, float* skip, const float* rs,
                                                              const float* mask, int H, int Th, int first,
-                                                             int last) {
+                                                             int last, unsigned* amax) {
   const int b = blockIdx.y;
   const int64_t n = (int64_t)H * Th;
+  float vm = 0.f;  // max |h| (not last: the next in_layer's input) or |skip| (last: the end conv's)
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int t = (int)(i % Th);
     const float m = mask[(size_t)b * Th + t];
     if (!last) {
       const float r0 = rs[(size_t)b * 2 * n + i];
       const float r1 = rs[(size_t)b * 2 * n + n + i];
-      h[(size_t)b * n + i] = (h[(size_t)b * n + i] + r0) * m;
+      const float hv = (h[(size_t)b * n + i] + r0) * m;
+      h[(size_t)b * n + i] = hv;
       skip[(size_t)b * n + i] = first ? r1 : skip[(size_t)b * n + i] + r1;
+      vm = fmaxf(vm, fabsf(hv));
     } else {
       const float r = rs[(size_t)b * n + i];
-      const float sk = first ? r : skip[(size_t)b * n + i] + r;
-      skip[(size_t)b * n + i] = sk * m;
+      const float sk = (first ? r : skip[(size_t)b * n + i] + r) * m;
+      skip[(size_t)b * n + i] = sk;
+      vm = fmaxf(vm, fabsf(sk));
     }
   }
+  if (amax) publish_amax(amax, b, vm);
 }
 
 // One thread per (b, group i, t).  Group i of InvConvNear (glow.py:116-117) holds channels
@@ -161,15 +173,15 @@ void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStrea
   TTS_HIP_CHECK(hipGetLastError());
 }
 
-void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s) {
-  hipLaunchKernelGGL(glow_gate_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, xin, acts, H, Th);
+void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s, unsigned* amax) {
+  hipLaunchKernelGGL(glow_gate_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, xin, acts, H, Th, amax);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H, int Th,
-                           int first, int last, hipStream_t s) {
+                           int first, int last, hipStream_t s, unsigned* amax) {
   hipLaunchKernelGGL(glow_wn_update_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, h, skip, rs, mask,
-                     H, Th, first, last);
+                     H, Th, first, last, amax);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

@@ -61,7 +61,6 @@ void vits_flow_validate(const TtsVitsFlowCfg& c) {
   }
   TTS_REQUIRE(c.cond_channels >= 0, 1, "cond_channels must be >= 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
-  TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3, "VITS flow: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
 VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device) : cfg_(cfg), device_(device) {
@@ -93,7 +92,7 @@ VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device
     const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);
     const size_t off = host.size();
     host.resize(off + align(n), 0.f);
-    pack_conv(mode, w, Cout, Cin, K, t, host.data() + off);
+    cv.w_exp = pack_conv(mode, w, Cout, Cin, K, t, host.data() + off);
     fix.push_back({off, &cv.w});
     const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
     const size_t offb = host.size();
@@ -156,12 +155,20 @@ VitsFlow::~VitsFlow() {
   if (ws_) (void)hipFree(ws_);
 }
 
+// f16x3 statistics: per flow (execution order) 2L + 2 groups of [B][64] slots: pre's input half,
+// h before each in_layer, acts before each res_skip layer, the final skip (post's input)
+size_t VitsFlow::amax_floats(int B) const {
+  if (cfg_.math_mode != MATH_FP32_F16X3) return 0;
+  return (size_t)cfg_.num_flows * (2 * cfg_.num_layers + 2) * B * 64;
+}
+
 void VitsFlow::reserve(int B, int T) {
   const int H = cfg_.hidden_channels;
   const size_t plane = (size_t)B * T;
   // h H, xin 2H, acts H, rs 2H, skip H; cond vectors [B][2*H*L]; odd num_flows: a C-channel copy
   const size_t odd = (cfg_.num_flows & 1) ? plane * cfg_.channels + 64 : 0;
-  const size_t need = (plane * 7 * H + (size_t)B * 2 * H * cfg_.num_layers + 64 * 8 + odd) * sizeof(float);
+  const size_t need =
+      (plane * 7 * H + (size_t)B * 2 * H * cfg_.num_layers + 64 * 8 + odd + amax_floats(B) + 64) * sizeof(float);
   if (need <= ws_bytes_) return;
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
@@ -187,6 +194,12 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
   float* rs = p; p += al(plane * 2 * H);
   float* skip = p; p += al(plane * H);
   float* cvec = p; p += al((size_t)B * 2 * H * L);
+  const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(p) : nullptr;
+  p += al(amax_floats(B));
+  const int ng = 2 * L + 2;
+  auto slots = [&](int fi, int kind) -> unsigned* { return h3 ? amax + ((size_t)fi * ng + kind) * B * 64 : nullptr; };
+  if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, amax_floats(B) * sizeof(unsigned), s));
   const bool odd = (cfg_.num_flows & 1) != 0;
   float* out = y;  // the flow updates `work` in place; an odd count flips it into y at the end
   float* work = odd ? p : y;
@@ -196,8 +209,10 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
   const int64_t xbs = (int64_t)C * T;  // batch stride of x / y
 
   auto conv = [&](const char* name, const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m,
-                  const float* res, int64_t o_bstride, const float* cv_vec, int64_t cv_bstride, bool mask_res) {
+                  const float* res, int64_t o_bstride, const float* cv_vec, int64_t cv_bstride, bool mask_res,
+                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
     Conv1dArgs a{};
+    a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = cv.w_exp;
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride; a.res = res;
     a.o_bstride = o_bstride; a.cvec = cv_vec; a.cvec_bstride = cv_bstride; a.mask_res = mask_res ? 1 : 0;
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = T; a.Tout = T;
@@ -213,20 +228,30 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
       run(prof, s, "vits_cond", 2.0 * B * 2 * H * L * cfg_.cond_channels, 4.0 * B * 2 * H * L,
           [&] { launch_cond_vec(g, Fl.cond_w, Fl.cond_b, cvec, B, cfg_.cond_channels, 2 * H * L, s); });
     }
+    const int fi = cfg_.num_flows - 1 - f;
+    const int half = C / 2;
+    if (h3)  // statistics of x0 (pre's input half), strided over the channel planes
+      run(prof, s, "vits_amax_x0", 0.0, 2.0 * P * half,
+          [&] { launch_amax(y + Fl.in_off * T, (int64_t)half * T, B, slots(fi, 0), s, xbs); });
     // h = pre(x0) * mask  (networks.py:157)
-    conv("vits_pre", Fl.pre, y + Fl.in_off * T, xbs, hb, mask, nullptr, 0, nullptr, 0, false);
+    conv("vits_pre", Fl.pre, y + Fl.in_off * T, xbs, hb, mask, nullptr, 0, nullptr, 0, false, slots(fi, 0),
+         slots(fi, 1));
     for (int l = 0; l < L; ++l) {
       // x_in = in_layers[l](h) (+ g_l)   (wavenet.py:101-107)
       conv("vits_wn_in", Fl.in_layers[l], hb, 0, xin, nullptr, nullptr, 0,
-           cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr, (int64_t)2 * H * L, false);
-      run(prof, s, "vits_gate", 0.0, 12.0 * P * H, [&] { launch_glow_gate(xin, acts, B, H, T, s); });  // :108
-      conv("vits_wn_res_skip", Fl.res_skip[l], acts, 0, rs, nullptr, nullptr, 0, nullptr, 0, false);  // :109
-      run(prof, s, "vits_wn_update", 0.0, 24.0 * P * H,
-          [&] { launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s); });  // :110-115
+           cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr, (int64_t)2 * H * L, false, slots(fi, 1 + l));
+      run(prof, s, "vits_gate", 0.0, 12.0 * P * H,
+          [&] { launch_glow_gate(xin, acts, B, H, T, s, slots(fi, 1 + L + l)); });  // :108
+      conv("vits_wn_res_skip", Fl.res_skip[l], acts, 0, rs, nullptr, nullptr, 0, nullptr, 0, false,
+           slots(fi, 1 + L + l));  // :109
+      run(prof, s, "vits_wn_update", 0.0, 24.0 * P * H, [&] {
+        launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s,
+                              l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
+      });  // :110-115
     }
     // x1 = (x1 - post(h) * mask) * mask, in place on y  (networks.py:159-165)
     float* x1 = y + Fl.out_off * T;
-    conv("vits_post", Fl.post, skip, 0, x1, mask, x1, xbs, nullptr, 0, true);
+    conv("vits_post", Fl.post, skip, 0, x1, mask, x1, xbs, nullptr, 0, true, slots(fi, 2 * L + 1));
   }
   if (odd) run(prof, s, "vits_flip", 0.0, 8.0 * P * C, [&] { launch_channel_flip(work, out, B, C, T, s); });
 }

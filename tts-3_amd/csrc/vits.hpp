@@ -25,7 +25,7 @@ class VitsFlow {
 
  private:
   struct Conv {
-    int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0;
+    int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0, w_exp = 0;
     float* w = nullptr;
     float* b = nullptr;
   };
@@ -38,6 +38,7 @@ class VitsFlow {
     int64_t out_off = 0;      // channel offset (x T) of the half the coupling updates
   };
   void reserve(int B, int T);
+  size_t amax_floats(int B) const;
 
   TtsVitsFlowCfg cfg_;
   int device_;
