@@ -75,8 +75,6 @@ constexpr ConvTile kSplitTiles[] = {
     {64, 128, 2, 1, 16, 1},   // 17
     {64, 128, 2, 1, 16, 2},   // 18
     {32, 512, 1, 4, 16, 2},   // 19
-    {128, 128, 1, 4, 32, 2},  // 20 waves stacked along Cout: each wave streams its own 32 weight
-    {128, 128, 1, 4, 16, 2},  // 21 rows (half the A fragments of the 2 x 2 layout), 4 B blocks
 };
 constexpr int kNumSplitTiles = sizeof(kSplitTiles) / sizeof(kSplitTiles[0]);
 

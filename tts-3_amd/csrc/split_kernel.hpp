@@ -262,8 +262,6 @@ void launch_split_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
     case 17: launch_split_t<S, K, 64, 128, 2, 1, 1, 1, false>(a, B, s); break;
     case 18: launch_split_t<S, K, 64, 128, 2, 1, 1, 2, false>(a, B, s); break;
     case 19: launch_split_t<S, K, 32, 512, 1, 4, 1, 2, false>(a, B, s); break;
-    case 20: launch_split_t<S, K, 128, 128, 1, 4, 2, 2, false>(a, B, s); break;
-    case 21: launch_split_t<S, K, 128, 128, 1, 4, 1, 2, false>(a, B, s); break;
     default: throw Error(3, "conv1d(split): bad tile index " + std::to_string(tile));
   }
 }
