@@ -216,6 +216,16 @@ def glow_bench(dev, math_mode, steps=10, warmup=3, B=16, T=768, cpu=True):
                             "achieved_tflops": fam["flops"] / fam["ms"] / 1e9, "launches": fam["n"]},
         "breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
     }
+    if math_mode != "fp32":  # the same flow in exact fp32 MFMA arithmetic, on the full bench input
+        d32 = Decoder(**cfg, dropout_p=G["dropout_p"], math_mode="fp32")
+        d32.load_state_dict(sd)
+        d32.eval()
+        d32.store_inverse()
+        d32 = d32.to(dev)
+        y, y32 = d(x, m, reverse=True)[0].double(), d32(x, m, reverse=True)[0].double()
+        out["vs_fp32_mode"] = {"max_abs": float((y - y32).abs().max()),
+                               "rel_rms": float((y - y32).pow(2).mean().sqrt() / y32.pow(2).mean().sqrt())}
+        del d32
     if cpu:
         sys.path.insert(0, REPO)
         from oracle import glow_ref  # test infrastructure: the baseline being timed, not the product
@@ -239,8 +249,8 @@ def glow_bench(dev, math_mode, steps=10, warmup=3, B=16, T=768, cpu=True):
 def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
     """Config 3: Glow-TTS (LJSpeech cfg) + HiFiGAN-v1 end to end, token ids -> waveform, B = 16 x 128
     tokens (durations ~6 frames/token from the synthetic predictor -> ~768 mel frames).
-    ``modes`` = (glow decoder mode, vocoder mode) per variant; the encoder always runs exact fp32
-    (its durations are ceil()-quantised, so they must match the reference's)."""
+    ``modes`` = (glow decoder mode, vocoder mode) per variant; the encoder always runs fp32x6, the
+    fp32-faithful mode (its durations are ceil()-quantised, so they must match the reference's)."""
     from tts_amd import synthetic
     from tts_amd.config import GLOW_TTS_DECODER as G, GLOW_TTS_ENCODER as E
     from tts_amd.synthesizer import AudioNorm, Synthesizer
@@ -257,7 +267,7 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
     tok = synthetic.tokens(B, T_x, 64, seed=11).to(dev)
     lens = torch.full((B,), T_x, dtype=torch.int64, device=dev)
     out = {"workload": f"Glow-TTS LJSpeech cfg + on-device hand-off (denormalize/normalize) + HiFiGAN-v1, "
-                       f"[{B} x {T_x}] token ids -> waveform (encoder fp32, noise_scale 0, length_scale 1)",
+                       f"[{B} x {T_x}] token ids -> waveform (encoder fp32x6, noise_scale 0, length_scale 1)",
            "variants": {}}
     for label, (dmode, vmode) in modes.items():
         m = GlowTTS(dict(num_chars=64), decoder_math_mode=dmode)

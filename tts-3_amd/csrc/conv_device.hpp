@@ -57,6 +57,20 @@ __device__ __forceinline__ void publish_amax(unsigned* slots, int b, float v) {
   if ((threadIdx.x & 63) == 0) atomicMax(slots + (size_t)b * 64 + (blockIdx.x & 63), __float_as_uint(v));
 }
 
+// Workgroup form for the grid-stride elementwise kernels (256 threads, called by every thread):
+// one atomic per workgroup instead of one per wave; thousands of per-wave atomics on an item's
+// two slot cache lines serialise in L2 and doubled the Glow gate / update kernels' time.
+__device__ __forceinline__ void publish_amax_block(unsigned* slots, int b, float v) {
+  __shared__ float red[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(slots + (size_t)b * 64 + (blockIdx.x & 63),
+              __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
 template <int TM, int TN, bool RES, int ZM, bool AMAX>
 __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
                                                    int tbase, int cobase, int lane, int tend) {

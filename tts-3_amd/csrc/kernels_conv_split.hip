@@ -38,11 +38,11 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     m = fmaxf(m, fabsf(xb[i]));
-  publish_amax(slots, blockIdx.z, m);
+  publish_amax_block(slots, blockIdx.z, m);
 }
 
 void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s, int64_t stride) {
-  const int64_t blocks = std::min<int64_t>(512, std::max<int64_t>(1, (n + 255) / 256));
+  const int64_t blocks = std::min<int64_t>(128, std::max<int64_t>(1, (n + 255) / 256));
   hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks, 1, B), dim3(256), 0, s, x, n, stride > 0 ? stride : n,
                      slots);
   TTS_HIP_CHECK(hipGetLastError());

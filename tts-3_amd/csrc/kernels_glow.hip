@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void glow_gate_kernel(const float* xin, float*
     acts[(size_t)b * n + i] = v;
     vm = fmaxf(vm, fabsf(v));
   }
-  if (amax) publish_amax(amax, b, vm);
+  if (amax) publish_amax_block(amax, b, vm);
 }
 
 // not last: h = (h + rs[:H]) * mask ; skip (+)= rs[H:]       last: skip = (skip + rs) * mask
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void glow_wn_update_kernel(float* h, float* sk
       vm = fmaxf(vm, fabsf(sk));
     }
   }
-  if (amax) publish_amax(amax, b, vm);
+  if (amax) publish_amax_block(amax, b, vm);
 }
 
 // One thread per (b, group i, t).  Group i of InvConvNear (glow.py:116-117) holds channels
@@ -134,9 +134,9 @@ __global__ __launch_bounds__(256) void glow_tail_kernel(GlowTailArgs a) {
 }
 
 namespace {
-dim3 ew_grid(int64_t n, int B) {
+dim3 ew_grid(int64_t n, int B, int64_t cap = 4096) {
   int64_t g = (n + 255) / 256;
-  if (g > 4096) g = 4096;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return dim3((unsigned)g, B);
 }
@@ -174,14 +174,16 @@ void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStrea
 }
 
 void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s, unsigned* amax) {
-  hipLaunchKernelGGL(glow_gate_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, xin, acts, H, Th, amax);
+  // with statistics: at most 128 workgroups per item (a few elements per thread, 128 atomics)
+  hipLaunchKernelGGL(glow_gate_kernel, ew_grid((int64_t)H * Th, B, amax ? 128 : 4096), dim3(256), 0, s, xin, acts,
+                     H, Th, amax);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H, int Th,
                            int first, int last, hipStream_t s, unsigned* amax) {
-  hipLaunchKernelGGL(glow_wn_update_kernel, ew_grid((int64_t)H * Th, B), dim3(256), 0, s, h, skip, rs, mask,
-                     H, Th, first, last, amax);
+  hipLaunchKernelGGL(glow_wn_update_kernel, ew_grid((int64_t)H * Th, B, amax ? 128 : 4096), dim3(256), 0, s, h,
+                     skip, rs, mask, H, Th, first, last, amax);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
