@@ -3,9 +3,20 @@
 // wavenet.py:94-115, normalization.py:88-103.
 #include "glow.hpp"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace tts {
+
+int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil) {
+  static const int forced = [] {
+    const char* e = std::getenv("TTS_MI355X_FLOW_TILE");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (is_split_mode(mode) && forced >= 0 && forced < conv_num_tiles(mode) && (K - 1) * dil <= (K - 1) * 5)
+    return forced;
+  return conv_tile_for(mode, Cout, K, Cin, dil, false);
+}
 
 std::vector<int64_t> glow_weight_shapes(const TtsGlowDecoderCfg& c) {
   std::vector<int64_t> n;
@@ -78,7 +89,7 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
     cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
     const int mode = cfg_.math_mode;
-    cv.tile = conv_tile_for(mode, Cout, K, Cin, dil, false);
+    cv.tile = flow_conv_tile(mode, Cout, K, Cin, dil);
     const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
     const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);

@@ -30,6 +30,11 @@ void launch_glow_squeeze(const float* x, const float* mask, float* xs, float* ms
 void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, int C, int Th, int nsq,
                            hipStream_t s);
 // amax: [B][64] max-abs slots of the output (f16x3 statistics of the next conv's input), or nullptr
+// Conv tile of the Glow / VITS flow convs (glow.cpp): the flows' column counts (B x T/2) are
+// small, so the split modes may take a smaller tile to fill the chip; TTS_MI355X_FLOW_TILE=<idx>
+// overrides it (A/B runs).
+int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil);
+
 void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s,
                       unsigned* amax = nullptr);
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,

@@ -86,7 +86,7 @@ VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device
   };
   auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
     cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
-    cv.tile = conv_tile_for(mode, Cout, K, Cin, dil, false);
+    cv.tile = flow_conv_tile(mode, Cout, K, Cin, dil);
     const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
     const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);
