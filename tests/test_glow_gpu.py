@@ -65,3 +65,23 @@ def test_glow_batch_invariance(cuda_device, mode):
     assert torch.equal(y[3], y1[0])
     y2, _ = d(x, m, reverse=True)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+def test_glow_gate_fusion_bitwise(cuda_device, mode, monkeypatch):
+    """The WN gate fused into the in_layer conv epilogue (kSplitGateTile) computes the same fp32
+    operations as the separate gate kernel: bitwise equal outputs, ragged mask included."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=3,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(3, 80, 301, generator=g).to(cuda_device)
+    m = (torch.arange(301)[None] < torch.tensor([301, 150, 9])[:, None]).float().unsqueeze(1).to(cuda_device)
+    outs, names = [], []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_FLOW_GATE", fused)
+        d = build(cfg, 23, cuda_device, mode)
+        outs.append(d(x, m, reverse=True)[0])
+        names.append({r["name"] for r in d.profile(x, m)[1]})
+    assert "glow_wn_in_gate" in names[0] and "glow_gate" not in names[0]
+    assert "glow_gate" in names[1] and "glow_wn_in_gate" not in names[1]
+    assert torch.equal(outs[0], outs[1])

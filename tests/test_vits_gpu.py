@@ -90,3 +90,21 @@ def test_vits_waveform_path(cuda_device, mode):
     assert_close_fp32(z.cpu(), zr, f"vits z ({mode})", **tol(mode))
     assert_close_fp32(wav.cpu(), wr, f"vits wav ({mode})", **tol(mode))
     assert np.isfinite(wav.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("cond", [0, 16])
+def test_vits_gate_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
+    """Gate fused into the in_layer epilogue, with the speaker term g_l (cvec, original row order)
+    added there: bitwise equal to the separate gate kernel."""
+    cfg = dict(VITS_FLOW, num_flows=2, cond_channels=cond)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(2, cfg["channels"], 257, generator=gen).to(cuda_device)
+    mask = (torch.arange(257)[None] < torch.tensor([257, 100])[:, None]).float().unsqueeze(1).to(cuda_device)
+    g = torch.randn(2, cond, 1, generator=gen).to(cuda_device) if cond else None
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_FLOW_GATE", fused)
+        f, _ = build(cfg, 31, cuda_device, mode)
+        outs.append(f(x, mask, g=g, reverse=True))
+    assert torch.equal(outs[0], outs[1])

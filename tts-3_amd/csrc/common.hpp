@@ -68,7 +68,20 @@ struct Conv1dArgs {
   int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
   int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
   int xcd_remap;         // split kernels: XCD-aware tile order (set by launch_conv1d_split)
+  // split tile kSplitGateTile only: the WaveNet gate fused into the epilogue (wavenet.py:6-13).
+  // gate = H: the packed rows interleave 64-row blocks of the tanh half (rows [0, H)) and the
+  // sigmoid half (rows [H, 2H)) (gate_row_order); y receives acts [B][H][Tout] =
+  // tanh(x_in[c]) * sigmoid(x_in[H + c]); bias is in packed row order, cvec in the original one.
+  int gate;
 };
+
+constexpr int kSplitGateTile = 20;  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
+// packed row rho of a gated in_layer -> original row: block j = rho / 128 holds tanh rows
+// [64j, 64j + 64) then sigmoid rows [H + 64j, H + 64j + 64) (H % 64 == 0)
+inline int gate_row_order(int rho, int H) {
+  const int j = rho / 128, r = rho % 128;
+  return r < 64 ? 64 * j + r : H + 64 * j + (r - 64);
+}
 
 // One fused ResBlock1 iteration (kernels_resblock.hip): c1 = convs1[m] (x, weights, dilation,
 // lrelu slopes, f16x3 input statistics), c2 = convs2[m] (weights, res = the iteration's input x,

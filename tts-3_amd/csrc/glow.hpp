@@ -34,6 +34,13 @@ void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, i
 // small, so the split modes may take a smaller tile to fill the chip; TTS_MI355X_FLOW_TILE=<idx>
 // overrides it (A/B runs).
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil);
+// Whether a WN in_layer (H -> 2H, kernel K, dilation dil) runs with the gate fused into its conv
+// epilogue (kSplitGateTile): split modes, H % 64 == 0, K in {3, 5, 7}, the tile's halo, and
+// TTS_MI355X_FLOW_GATE=1 at create time (opt-in: measured slower end to end at config 3).
+bool flow_gate_fused(int mode, int H, int K, int dil);
+// in_layer weights [2H][H][K] and bias [2H] in gate_row_order (for kSplitGateTile)
+void gate_permute_rows(const float* w, const float* b, int H, int Cin, int K, std::vector<float>& wp,
+                       std::vector<float>& bp);
 
 void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipStream_t s,
                       unsigned* amax = nullptr);
@@ -55,6 +62,7 @@ class GlowDecoder {
  private:
   struct Conv {
     int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0, w_exp = 0;
+    bool gated = false;  // in_layer with the WN gate fused (kSplitGateTile)
     float* w = nullptr;
     float* b = nullptr;
   };

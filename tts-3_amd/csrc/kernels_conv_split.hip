@@ -75,7 +75,9 @@ constexpr ConvTile kSplitTiles[] = {
     {64, 128, 2, 1, 16, 1},   // 17
     {64, 128, 2, 1, 16, 2},   // 18
     {32, 512, 1, 4, 16, 2},   // 19
+    {128, 128, 2, 2, 32, 2},  // 20 = kSplitGateTile: 13 with the WaveNet gate epilogue
 };
+static_assert(kSplitGateTile == 20, "tile table");
 constexpr int kNumSplitTiles = sizeof(kSplitTiles) / sizeof(kSplitTiles[0]);
 
 }  // namespace

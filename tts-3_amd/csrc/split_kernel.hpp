@@ -24,12 +24,82 @@ struct SplitCfg {
 #define X6_ABLATE 0  // ablation builds (scripts/gpu_ablate.sh): 1 no staging refill, 2 no A stream
 #endif
 
-template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD>
+// WaveNet gate epilogue (Conv1dArgs::gate, 128 x 128 tiles with 2 x 2 waves): the wm = 1 waves
+// hold the sigmoid rows matching the wm = 0 waves' tanh rows, column for column; they pass
+// sigmoid(v) through LDS (the staging buffers, free after the last chunk) and the wm = 0 waves
+// store tanh(v) * sigmoid and publish its max-abs.  Same fp32 operations, in the same order, as
+// the plain epilogue followed by glow_gate_kernel, so the result is bitwise that of the unfused pair.
+constexpr int C_WN_MAX = 2;  // column-group waves of the gate tile (2 x 2 waves)
+
+template <int TM, int TN, bool H3>
+__device__ __forceinline__ void gate_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b, int tbase,
+                                              int mt, int wm, int wn, int lane, float* xch) {
+  static_assert(TM * 32 == 64, "a wave row block must be one 64-row half");
+  const Conv1dArgs a = args;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int H = a.gate;
+  const int T = a.Tout;
+  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)(2 * H) * 4u);
+  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)2 * H) : a.bias,
+                               a.cvec ? (unsigned)(2 * H) * 4u : 0u);
+  const int orow0 = (wm ? H : 0) + 64 * mt;  // original row of this wave's local row 0
+  const int prow0 = mt * 128 + wm * 64;      // packed row
+  float v[TM][TN][16];
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+      const float bv = bload(rbias, (unsigned)(prow0 + rr) * 4u, 0u) + bload(rcv, (unsigned)(orow0 + rr) * 4u, 0u);
+#pragma unroll
+      for (int n = 0; n < TN; ++n) v[m][n][r] = lrelu2((acc[m][n][r] + bv) * 1.f, 1.f);
+    }
+  }
+  static_assert(TN == 2, "the two row-block waves split the output columns n = 0 / 1");
+  // both waves of a column group evaluate their own half (wm = 0: tanh, wm = 1: sigmoid), hand the
+  // half of the partner's columns over through LDS, and finish one column block each
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[m][n][r] = wm ? 1.f / (1.f + expf(-v[m][n][r])) : tanhf(v[m][n][r]);
+  const int give = 1 - wm;  // the column block the partner finishes
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xch[(((wm * C_WN_MAX + wn) * TM + m) * 16 + r) * 64 + lane] = give ? v[m][1][r] : v[m][0][r];
+  __syncthreads();
+  const int nk = wm;  // the column block this wave finishes
+  const unsigned rowb = (unsigned)T * 4u;
+  const rsrc_t rout = make_rsrc(a.y + (size_t)b * H * T, (unsigned)H * rowb);
+  const int t = tbase + nk * 32 + l32;
+  const unsigned voff0 = t < T ? (unsigned)t * 4u : OOB_OFF;
+  float vm = 0.f;
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const unsigned voff = t < T ? voff0 + (unsigned)(64 * mt + m * 32 + 4 * half) * rowb : OOB_OFF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float mine = nk ? v[m][1][r] : v[m][0][r];
+      const float other = xch[((((1 - wm) * C_WN_MAX + wn) * TM + m) * 16 + r) * 64 + lane];
+      const float o = (wm ? other : mine) * (wm ? mine : other);  // tanh * sigmoid, as glow_gate_kernel
+      if (H3) vm = t < T ? fmaxf(vm, fabsf(o)) : vm;
+      bstore(rout, o, voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u);
+    }
+  }
+  if (H3 && a.amax_out) publish_amax(a.amax_out, b, vm);
+}
+
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD, bool GATE = false>
 __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   using C = SplitCfg<S, K, BM, BN, TM, TN, G, HMAX, PD>;
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB];
+  // the gate epilogue reuses the staging buffers for its sigmoid exchange (32 KiB)
+  constexpr int XCHB = GATE ? 4 * C::WN * TM * TN * 16 * 64 : 0;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB > XCHB ? 2 * C::XSZB : XCHB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -218,7 +288,10 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
 #pragma unroll
       for (int n = 0; n < TN; ++n) acc[0][m][n] *= sc;
   }
-  if constexpr (K == 2) {
+  if constexpr (GATE) {
+    static_assert(BM == 128 && C::WM == 2, "gate epilogue");
+    gate_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt, wm, wn, lane, reinterpret_cast<float*>(smem));
+  } else if constexpr (K == 2) {
     convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
   } else {
     conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
@@ -226,10 +299,19 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
 }
 
 namespace split_detail {
-template <class S, int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE>
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE, bool GATE = false>
 void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
   const int halo = (K - 1) * a.dil;
+  if constexpr (GATE) {
+    TTS_REQUIRE(a.gate > 0 && a.gate % 64 == 0 && a.Cout == 2 * a.gate && a.zmode == 0 && !a.res && !a.mask &&
+                    a.ups == 0 && halo <= (K - 1) * 5,
+                1, "conv1d(split): bad gated in_layer arguments");
+    hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD, true>), grid, dim3(256), 0, s,
+                       a);
+    return;
+  }
+  TTS_REQUIRE(a.gate == 0, 1, "conv1d(split): the gate epilogue needs tile kSplitGateTile");
   if (halo <= (K - 1) * 5) {
     hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD>), grid, dim3(256), 0, s, a);
   } else if (WIDE && halo <= 96) {
@@ -262,6 +344,10 @@ void launch_split_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
     case 17: launch_split_t<S, K, 64, 128, 2, 1, 1, 1, false>(a, B, s); break;
     case 18: launch_split_t<S, K, 64, 128, 2, 1, 1, 2, false>(a, B, s); break;
     case 19: launch_split_t<S, K, 32, 512, 1, 4, 1, 2, false>(a, B, s); break;
+    case kSplitGateTile:
+      if constexpr (K == 3 || K == 5 || K == 7) launch_split_t<S, K, 128, 128, 2, 2, 2, 2, false, true>(a, B, s);
+      else throw Error(3, "conv1d(split): the gated in_layer takes kernel size 3, 5 or 7");
+      break;
     default: throw Error(3, "conv1d(split): bad tile index " + std::to_string(tile));
   }
 }

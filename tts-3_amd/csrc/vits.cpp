@@ -84,9 +84,18 @@ VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device
     std::memcpy(host.data() + off, src, n * sizeof(float));
     fix.push_back({off, dst});
   };
-  auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil) {
+  std::vector<float> wperm, bperm;
+  auto put_conv = [&](Conv& cv, const float* w, const float* b, int Cin, int Cout, int K, int dil,
+                      bool gate = false) {
     cv.Cin = Cin; cv.Cout = Cout; cv.K = K; cv.dil = dil;
     cv.tile = flow_conv_tile(mode, Cout, K, Cin, dil);
+    cv.gated = gate && flow_gate_fused(mode, Cout / 2, K, dil);
+    if (cv.gated) {
+      gate_permute_rows(w, b, Cout / 2, Cin, K, wperm, bperm);
+      w = wperm.data();
+      b = bperm.data();
+      cv.tile = kSplitGateTile;
+    }
     const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
     const size_t n = packed_conv_numel(mode, Cout, Cin, K, t);
@@ -120,7 +129,7 @@ VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device
     Fl.res_skip.resize(L);
     int d = 1;
     for (int l = 0; l < L; ++l) {
-      put_conv(Fl.in_layers[l], hw[wi], hw[wi + 1], H, 2 * H, cfg_.kernel_size, d);
+      put_conv(Fl.in_layers[l], hw[wi], hw[wi + 1], H, 2 * H, cfg_.kernel_size, d, true);
       wi += 2;
       d *= cfg_.dilation_rate;
     }
@@ -212,6 +221,7 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
                   const float* res, int64_t o_bstride, const float* cv_vec, int64_t cv_bstride, bool mask_res,
                   const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
     Conv1dArgs a{};
+    a.gate = cv.gated ? cv.Cout / 2 : 0;
     a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = cv.w_exp;
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride; a.res = res;
     a.o_bstride = o_bstride; a.cvec = cv_vec; a.cvec_bstride = cv_bstride; a.mask_res = mask_res ? 1 : 0;
@@ -238,10 +248,16 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
          slots(fi, 1));
     for (int l = 0; l < L; ++l) {
       // x_in = in_layers[l](h) (+ g_l)   (wavenet.py:101-107)
-      conv("vits_wn_in", Fl.in_layers[l], hb, 0, xin, nullptr, nullptr, 0,
-           cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr, (int64_t)2 * H * L, false, slots(fi, 1 + l));
-      run(prof, s, "vits_gate", 0.0, 12.0 * P * H,
-          [&] { launch_glow_gate(xin, acts, B, H, T, s, slots(fi, 1 + L + l)); });  // :108
+      const float* gl = cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr;
+      if (Fl.in_layers[l].gated) {  // in_layer + g_l + gate (:108) in one launch
+        conv("vits_wn_in_gate", Fl.in_layers[l], hb, 0, acts, nullptr, nullptr, 0, gl, (int64_t)2 * H * L, false,
+             slots(fi, 1 + l), slots(fi, 1 + L + l));
+      } else {
+        conv("vits_wn_in", Fl.in_layers[l], hb, 0, xin, nullptr, nullptr, 0, gl, (int64_t)2 * H * L, false,
+             slots(fi, 1 + l));
+        run(prof, s, "vits_gate", 0.0, 12.0 * P * H,
+            [&] { launch_glow_gate(xin, acts, B, H, T, s, slots(fi, 1 + L + l)); });  // :108
+      }
       conv("vits_wn_res_skip", Fl.res_skip[l], acts, 0, rs, nullptr, nullptr, 0, nullptr, 0, false,
            slots(fi, 1 + L + l));  // :109
       run(prof, s, "vits_wn_update", 0.0, 24.0 * P * H, [&] {

@@ -26,6 +26,7 @@ class VitsFlow {
  private:
   struct Conv {
     int Cin = 0, Cout = 0, K = 1, dil = 1, tile = 0, n_chunks = 0, w_exp = 0;
+    bool gated = false;  // in_layer with the WN gate fused (kSplitGateTile)
     float* w = nullptr;
     float* b = nullptr;
   };
