@@ -239,7 +239,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
     const Flow& F = flows_[f];
     const int fi = cfg_.num_flow_blocks - 1 - f;
-    if (h3)  // statistics of x_0 (the start conv's input), strided over the squeezed channels
+    if (h3 && fi == 0)  // statistics of x_0 (the start conv's input); later flows: the previous tail
       run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
@@ -262,6 +262,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
     GlowTailArgs ta{};
     ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
     ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
+    ta.amax_x0 = (h3 && f > 0) ? slots(fi + 1, 0) : nullptr;
     run(prof, s, "glow_tail", 0.0, 16.0 * P * C2, [&] { launch_glow_tail(ta, B, s); });
   }
   if (nsq > 1) {

@@ -24,6 +24,8 @@ struct GlowTailArgs {
   const float* bias;   // [C2]
   int C2, Th, S;
   int sigmoid_scale;
+  unsigned* amax_x0;   // [B][64] slots receiving max |x[:, :C2/2]| after the update (the next flow's
+                       // start-conv input, f16x3), or nullptr
 };
 void launch_glow_squeeze(const float* x, const float* mask, float* xs, float* msq, int B, int C, int T,
                          int nsq, hipStream_t s);

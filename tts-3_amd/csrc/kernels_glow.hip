@@ -99,6 +99,7 @@ __global__ __launch_bounds__(256) void glow_tail_kernel(GlowTailArgs a) {
   for (int o = 0; o < S; ++o)
 #pragma unroll
     for (int g = 0; g < S; ++g) W[o][g] = a.winv[o * S + g];
+  float vm = 0.f;  // max |x_0| of the updated x (the next flow's statistics)
   for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
     const int t = (int)(e % Th);
     const int i = (int)(e / Th);
@@ -129,8 +130,10 @@ __global__ __launch_bounds__(256) void glow_tail_kernel(GlowTailArgs a) {
       const int ch = chs[o];
       v = (v - a.bias[ch]) * expf(-a.logs[ch]) * m;                   // ActNorm reverse
       a.x[((size_t)b * C2 + ch) * Th + t] = v;
+      if (ch < half) vm = fmaxf(vm, fabsf(v));
     }
   }
+  if (a.amax_x0) publish_amax_block(a.amax_x0, b, vm);
 }
 
 namespace {
@@ -189,10 +192,11 @@ void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* 
 
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s) {
   const int64_t n = (int64_t)(a.C2 / a.S) * a.Th;
+  const int64_t cap = a.amax_x0 ? 128 : 4096;  // with statistics: one atomic per workgroup, <= 128 per item
   switch (a.S) {
-    case 2: hipLaunchKernelGGL(glow_tail_kernel<2>, ew_grid(n, B), dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(glow_tail_kernel<4>, ew_grid(n, B), dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(glow_tail_kernel<8>, ew_grid(n, B), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(glow_tail_kernel<2>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(glow_tail_kernel<4>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(glow_tail_kernel<8>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
     default: throw Error(3, "InvConvNear num_splits must be 2, 4 or 8");
   }
   TTS_HIP_CHECK(hipGetLastError());
