@@ -85,3 +85,22 @@ def test_glow_gate_fusion_bitwise(cuda_device, mode, monkeypatch):
     assert "glow_wn_in_gate" in names[0] and "glow_gate" not in names[0]
     assert "glow_gate" in names[1] and "glow_wn_in_gate" not in names[1]
     assert torch.equal(outs[0], outs[1])
+
+
+def test_glow_x0_statistics_match_prepass(cuda_device, monkeypatch):
+    """f16x3: every flow's x0 max-abs published by the previous flow's tail kernel equals the
+    strided pre-pass it replaced (TTS_MI355X_FLOW_AMAX_PREPASS=1): bitwise equal outputs, ragged
+    masks included.  An under-reported max would overflow fp16 and show up here first."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=4,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    g = torch.Generator().manual_seed(29)
+    x = (torch.randn(3, 80, 257, generator=g) * 3).to(cuda_device)
+    m = (torch.arange(257)[None] < torch.tensor([257, 120, 7])[:, None]).float().unsqueeze(1).to(cuda_device)
+    outs, names = [], []
+    for prepass in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_FLOW_AMAX_PREPASS", prepass)
+        d = build(cfg, 41, cuda_device, "f16x3")
+        outs.append(d(x, m, reverse=True)[0])
+        names.append([r["name"] for r in d.profile(x, m)[1]])
+    assert names[0].count("glow_amax_x0") == 4 and names[1].count("glow_amax_x0") == 1
+    assert torch.equal(outs[0], outs[1])

@@ -76,6 +76,20 @@ def test_wav_int16_matches_save_wav_scaling(cuda_device):
 HRANGE = goldens("handoff_range")
 
 
+def test_wav_int16_nonfinite_matches_numpy(cuda_device):
+    """NaN / inf / overflowing samples follow numpy's x86 behaviour (see kernels_handoff.hip)."""
+    rng = np.random.default_rng(5)
+    w = (np.tanh(rng.standard_normal((3, 1, 4099))) * 0.7).astype(np.float32)
+    w[0, 0, 17] = np.nan  # scale 32767 / 0.01: most samples wrap
+    w[1, 0, 4000] = np.inf  # scale 0: finite -> 0, inf -> NaN -> 0
+    w[2, 0, 5] = -np.inf
+    w[2, 0, 9] = np.nan
+    out = wav_to_int16(torch.from_numpy(w).to(cuda_device)).cpu().numpy()
+    with np.errstate(invalid="ignore", over="ignore"):
+        for b in range(3):
+            assert np.array_equal(out[b], handoff_ref.wav_int16(w[b, 0])), b
+
+
 @pytest.mark.parametrize("name,meta,arr", HRANGE, ids=[g[0] for g in HRANGE])
 def test_handoff_and_int16_vs_reference_functions(cuda_device, name, meta, arr):
     """Bit-exact against the reference's own AudioProcessor.normalize/denormalize and

@@ -82,6 +82,58 @@ def test_op_conv1d(cuda_device, case, mode):
     assert_close_fp32(out.cpu(), ref, f"conv1d {case}", **tol(mode))
 
 
+WINO_TILE = 21  # kSplitWinoTile (common.hpp): Winograd F(4,4), f16x3
+WINO_CASES = [
+    # B, Cin, Cout, T, K, dil, in_slope, out_slope, res, zmode
+    (2, 256, 256, 300, 11, 5, 0.1, 0.1, False, 0),   # stage-1 convs1
+    (1, 128, 128, 1000, 7, 3, 0.1, 0.1, False, 0),   # stage-2 convs1
+    (1, 128, 128, 777, 11, 1, 1.0, 1.0, True, 2),    # convs2 + residual, z accumulate
+    (2, 256, 256, 129, 7, 1, 1.0, 1.0, True, 3),     # z final (/3)
+    (1, 128, 128, 1, 11, 5, 0.1, 0.1, False, 0),     # single frame
+    (2, 128, 128, 9, 7, 5, 0.1, 0.1, True, 1),       # shorter than the halo
+    (3, 144, 256, 263, 11, 3, 0.1, 1.0, True, 0),    # Cin != Cout, 9 channel chunks
+    (1, 128, 384, 1283, 11, 1, 0.1, 0.1, False, 0),  # 3 row blocks, ragged last workgroup
+]
+
+
+@pytest.mark.parametrize("case", WINO_CASES, ids=[f"w{i}" for i in range(len(WINO_CASES))])
+def test_op_conv1d_winograd(cuda_device, case):
+    """The Winograd F(4,4) conv (wino_kernel.hpp) against fp64 at the fp32 gates, every epilogue
+    mode, every dilation, lengths around its 256 / 252 / 240-sample workgroups."""
+    B, Cin, Cout, T, K, dil, s_in, s_out, use_res, zmode = case
+    g = _rng(hash(case) & 0xFFFF)
+    x = torch.randn(B, Cin, T, generator=g) * 2
+    w = torch.randn(Cout, Cin, K, generator=g) / np.sqrt(Cin * K)
+    b = torch.randn(Cout, generator=g) * 0.1
+    res = torch.randn(B, Cout, T, generator=g) if use_res else None
+    z0 = torch.randn(B, Cout, T, generator=g)
+    v = F.conv1d(F.leaky_relu(x.double(), s_in), w.double(), b.double(), dilation=dil, padding=dil * (K - 1) // 2)
+    v = F.leaky_relu(v, s_out)
+    if res is not None:
+        v = v + res.double()
+    ref = {0: v, 1: v, 2: z0.double() + v, 3: (z0.double() + v) / 3.0}[zmode]
+    d = N.TtsConv1dDesc(B, Cin, Cout, T, K, dil, 0, s_in, s_out, zmode, 3.0, N.MATH_MODES["f16x3"])
+    y = torch.full((B, Cout, T), float("nan"), device=cuda_device)
+    z = z0.to(cuda_device)
+    resd = res.to(cuda_device) if res is not None else None
+    wn, bn = w.numpy().copy(), b.numpy().copy()
+    N.call("tts_op_conv1d_bench", ctypes.byref(d), N.ptr(x.to(cuda_device)), N.ptr(wn), N.ptr(bn), N.ptr(resd),
+           N.ptr(y), N.ptr(z), WINO_TILE, 0, None, N.stream_ptr(cuda_device))
+    out = y if zmode == 0 else z
+    ma, rr = assert_close_fp32(out.cpu(), ref, f"winograd conv1d {case}")
+    assert rr < 3e-6, rr  # ~3x the direct f16x3 conv's error, far inside the gate
+
+
+def test_op_conv1d_winograd_rejects_unsupported(cuda_device):
+    x = torch.zeros(1, 120, 16, device=cuda_device)
+    y = torch.zeros(1, 128, 16, device=cuda_device)
+    w, b = np.zeros((128, 120, 11), np.float32), np.zeros(128, np.float32)
+    d = N.TtsConv1dDesc(1, 120, 128, 16, 11, 1, 0, 1.0, 1.0, 0, 1.0, N.MATH_MODES["f16x3"])  # Cin % 16 != 0
+    with pytest.raises(N.NativeError):
+        N.call("tts_op_conv1d_bench", ctypes.byref(d), N.ptr(x), N.ptr(w), N.ptr(b), None, N.ptr(y), None,
+               WINO_TILE, 0, None, N.stream_ptr(cuda_device))
+
+
 # ----------------------------------------------------------------------------- conv_transpose1d
 CONVT_CASES = [
     # B, Cin, Cout, T, U
@@ -231,13 +283,15 @@ def test_benchmark_size_properties(cuda_device, mode):
     assert_close_fp32(out[17:18].cpu(), ref, "B=32 item 17 vs fp64 oracle", **tol(mode))
 
 
-def test_split_modes_accuracy_not_worse_than_fp32(cuda_device):
+def test_split_modes_accuracy_not_worse_than_fp32(cuda_device, monkeypatch):
     """The bf16x6 and scaled fp16 hi/lo splits are fp32-faithful: their error vs the fp64
-    reference matches exact-fp32 MFMA (and the reference's own fp32 CPU forward)."""
+    reference matches exact-fp32 MFMA (and the reference's own fp32 CPU forward).  The Winograd
+    F(4,4) form of the >= 128-channel MRF convs (f16x3 default) stays within 4x of it."""
     name, meta, arr = [h for h in HIFI if h[0] == "hifigan_v1_b2_t32"][0]
     errs = {}
-    for mode in ("fp32", "fp32x6", "f16x3"):
-        g = build(meta["config"], meta["seed"], cuda_device, mode)
+    for mode, wino in (("fp32", "0"), ("fp32x6", "0"), ("f16x3", "0"), ("f16x3_wino", "all")):
+        monkeypatch.setenv("TTS_MI355X_WINO", wino)
+        g = build(meta["config"], meta["seed"], cuda_device, mode.split("_")[0])
         out = g.inference(torch.from_numpy(arr["mel"]).to(cuda_device)).cpu().numpy()
         errs[mode] = (max_abs(out, arr["out_ref_fp64"]), rel_rms(out, arr["out_ref_fp64"]))
     ref32 = (max_abs(arr["out_ref_fp32"], arr["out_ref_fp64"]), rel_rms(arr["out_ref_fp32"], arr["out_ref_fp64"]))
@@ -245,3 +299,23 @@ def test_split_modes_accuracy_not_worse_than_fp32(cuda_device):
     for mode in ("fp32x6", "f16x3"):
         assert errs[mode][1] <= 2.0 * max(errs["fp32"][1], ref32[1]), mode
         assert errs[mode][0] <= 2.0 * max(errs["fp32"][0], ref32[0]), mode
+    assert errs["f16x3_wino"][1] <= 4.0 * max(errs["fp32"][1], ref32[1])
+    assert errs["f16x3_wino"][0] <= 4.0 * max(errs["fp32"][0], ref32[0])
+
+
+def test_winograd_generator_matches_direct(cuda_device, monkeypatch):
+    """Whole HiFiGAN-v1 with and without the Winograd MRF convs (f16x3) at a multi-workgroup
+    length: both within the fp32 gates of the fp64 oracle and of each other."""
+    sd = synthetic.hifigan_state_dict(seed=77, weight_norm=False)
+    mel = synthetic.mel(2, 61, seed=5)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    outs = []
+    for wino in ("all", "1", "0"):  # every supported MRF conv / the default selection / none
+        monkeypatch.setenv("TTS_MI355X_WINO", wino)
+        g = HifiganGenerator(**V1, math_mode="f16x3")
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs.append(g.inference(mel.to(cuda_device)).cpu())
+        assert_close_fp32(outs[-1], ref, f"wino={wino}")
+    assert max_abs(outs[0].numpy(), outs[2].numpy()) < 2e-5 and max_abs(outs[1].numpy(), outs[2].numpy()) < 2e-5

@@ -215,3 +215,16 @@ def test_handoff_range_oracle_matches_reference(name, meta, arr):
         assert out.dtype == np.float32 and np.array_equal(out, arr[f"out_{i}_{j}"]), (i, j)
     for k in range(meta["n_wavs"]):
         assert np.array_equal(handoff_ref.wav_int16(arr[f"wav_{k}"]), arr[f"pcm_{k}"]), k
+
+
+def test_wav_int16_nonfinite_contract():
+    """save_wav (numpy_transforms.py:436-438) on non-finite samples, as numpy does it on x86: a NaN
+    makes np.max NaN and max(0.01, nan) = 0.01; the int16 cast goes through int32 (NaN, inf and
+    |v| >= 2^31 -> INT_MIN -> 0) and wraps.  tts_wav_to_int16 implements exactly this contract."""
+    from oracle import handoff_ref
+
+    with np.errstate(invalid="ignore", over="ignore"):
+        w = np.array([0.5, np.nan, -0.2, np.inf, 1e-3, 700.0], dtype=np.float32)
+        assert handoff_ref.wav_int16(w).tolist() == [-50, 0, 20, 0, 3276, 0]  # scale 32767 / 0.01
+        w = np.array([0.5, -0.2, -np.inf, 0.0], dtype=np.float32)  # max = inf: scale 0, inf * 0 = NaN
+        assert handoff_ref.wav_int16(w).tolist() == [0, 0, 0, 0]

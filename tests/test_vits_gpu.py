@@ -108,3 +108,20 @@ def test_vits_gate_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
         f, _ = build(cfg, 31, cuda_device, mode)
         outs.append(f(x, mask, g=g, reverse=True))
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cond", [0, 16])
+def test_vits_x0_statistics_match_prepass(cuda_device, cond, monkeypatch):
+    """f16x3: the next flow's x0 max-abs from the post conv epilogue equals the per-flow pre-pass
+    (TTS_MI355X_FLOW_AMAX_PREPASS=1): bitwise equal outputs with a ragged mask."""
+    cfg = dict(VITS_FLOW, num_flows=4, cond_channels=cond)
+    gen = torch.Generator().manual_seed(8)
+    x = (torch.randn(2, cfg["channels"], 211, generator=gen) * 2).to(cuda_device)
+    mask = (torch.arange(211)[None] < torch.tensor([211, 64])[:, None]).float().unsqueeze(1).to(cuda_device)
+    g = torch.randn(2, cond, 1, generator=gen).to(cuda_device) if cond else None
+    outs = []
+    for prepass in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_FLOW_AMAX_PREPASS", prepass)
+        f, _ = build(cfg, 37, cuda_device, "f16x3")
+        outs.append(f(x, mask, g=g, reverse=True))
+    assert torch.equal(outs[0], outs[1])

@@ -75,7 +75,14 @@ struct Conv1dArgs {
   int gate;
 };
 
-constexpr int kSplitGateTile = 20;  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
+constexpr int kSplitGateTile = 20;
+constexpr int kSplitWinoTile = 21;  // Winograd F(4,4), 128 rows x 64 tile columns (wino_kernel.hpp)
+// Winograd F(4,4) conv (kernels_conv_wino.hip): f16x3, Cout % 128 == 0, Cin % 16 == 0, K in {7, 11},
+// dilation 1/3/5, no mask / replicate padding / gate / ConvTranspose form
+bool wino_supported(int mode, int Cout, int Cin, int K, int dil);
+bool wino_enabled();
+bool wino_all();
+void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s);  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
 // packed row rho of a gated in_layer -> original row: block j = rho / 128 holds tanh rows
 // [64j, 64j + 64) then sigmoid rows [H + 64j, H + 64j + 64) (H % 64 == 0)
 inline int gate_row_order(int rho, int H) {
@@ -116,6 +123,7 @@ void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_
 struct ConvTile {
   int BM, BN, TM, TN, CK;
   int PD = 1;
+  int WINO = 0;  // Winograd F(4,4) kernel (wino_kernel.hpp): weights packed as 7*ceil(K/4) steps
 };
 
 // Polyphase ConvTranspose1d, K == 2*U, padding U/2: every output phase s is a dense
@@ -192,18 +200,21 @@ int64_t packed_conv1d_numel(int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] -> [Cout_pad/BM][n_chunks][2U][CK][BM].
 void pack_convT(const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out);
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t);
-// Split modes: [mblock32][cgroup16][K][piece][64][8 x 16-bit] (+2 steps of slack).  Returns the
+// Split modes: [mblock32][cgroup16][K][piece][64][8 x 16-bit] (+4 steps of slack).  Returns the
 // exponent e with which the weights were pre-scaled by 2^-e (0 for bf16x6).
 int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
 int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] as the K=2 conv of Conv1dArgs::ups (U*Cout rows);
 // returns w_exp.  Its bias is the conv's bias repeated per phase: bias'[co*U + s] = bias[co].
 int pack_convT_split(int mode, const float* w, int Cin, int Cout, int U, const ConvTile& t, float* out);
+int pack_conv1d_wino(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
 inline int64_t packed_conv_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
+  if (t.WINO) return packed_conv1d_split_numel(mode, Cout, Cin, 7 * ((K + 3) / 4), t);
   return is_split_mode(mode) ? packed_conv1d_split_numel(mode, Cout, Cin, K, t) : packed_conv1d_numel(Cout, Cin, K, t);
 }
 // returns the weight scale exponent (Conv1dArgs::w_exp)
 inline int pack_conv(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
+  if (t.WINO) return pack_conv1d_wino(mode, w, Cout, Cin, K, t, out);
   if (is_split_mode(mode)) return pack_conv1d_split(mode, w, Cout, Cin, K, t, out);
   pack_conv1d(w, Cout, Cin, K, t, out);
   return 0;

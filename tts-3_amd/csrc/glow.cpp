@@ -26,6 +26,11 @@ bool flow_gate_fused(int mode, int H, int K, int dil) {
   return is_split_mode(mode) && H % 64 == 0 && (K == 3 || K == 5 || K == 7) && (K - 1) * dil <= (K - 1) * 5;
 }
 
+bool flow_amax_prepass() {
+  const char* e = std::getenv("TTS_MI355X_FLOW_AMAX_PREPASS");
+  return e && e[0] == '1';
+}
+
 void gate_permute_rows(const float* w, const float* b, int H, int Cin, int K, std::vector<float>& wp,
                        std::vector<float>& bp) {
   const size_t row = (size_t)Cin * K;
@@ -87,6 +92,7 @@ void glow_validate(const TtsGlowDecoderCfg& c) {
 GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, int device)
     : cfg_(cfg), device_(device) {
   glow_validate(cfg_);
+  amax_prepass_ = flow_amax_prepass();
   DeviceGuard g(device_);
   const auto shapes = glow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -239,7 +245,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
     const Flow& F = flows_[f];
     const int fi = cfg_.num_flow_blocks - 1 - f;
-    if (h3 && fi == 0)  // statistics of x_0 (the start conv's input); later flows: the previous tail
+    if (h3 && (fi == 0 || amax_prepass_))  // statistics of x_0 (the start conv's input); later flows: the previous tail
       run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
@@ -262,7 +268,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
     GlowTailArgs ta{};
     ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
     ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
-    ta.amax_x0 = (h3 && f > 0) ? slots(fi + 1, 0) : nullptr;
+    ta.amax_x0 = (h3 && f > 0 && !amax_prepass_) ? slots(fi + 1, 0) : nullptr;
     run(prof, s, "glow_tail", 0.0, 16.0 * P * C2, [&] { launch_glow_tail(ta, B, s); });
   }
   if (nsq > 1) {

@@ -113,6 +113,12 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
     L.mode = lmode;
     L.tile = conv_tile_for(lmode, Cout, K, Cin, dil, res);
+    // the MRF convs at >= 128 channels: Winograd F(4,4) where it measured faster than the direct
+    // kernel on MI355X (wino_kernel.hpp; kernel 11 at 128/256 channels, kernel 7 at 256;
+    // TTS_MI355X_WINO=0 off, =all every supported conv)
+    if (std::string(fam) == "mrf_conv" && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil) &&
+        (K == 11 || Cout >= 256 || wino_all()))
+      L.tile = kSplitWinoTile;
     const ConvTile t = conv_tile(lmode, L.tile);
     L.n_chunks = ceil_div(Cin, t.CK);
     L.w_numel = packed_conv_numel(lmode, Cout, Cin, K, t);

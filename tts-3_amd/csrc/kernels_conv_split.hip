@@ -76,8 +76,9 @@ constexpr ConvTile kSplitTiles[] = {
     {64, 128, 2, 1, 16, 2},   // 18
     {32, 512, 1, 4, 16, 2},   // 19
     {128, 128, 2, 2, 32, 2},  // 20 = kSplitGateTile: 13 with the WaveNet gate epilogue
+    {128, 64, 1, 2, 16, 2, 1},  // 21 = kSplitWinoTile: Winograd F(4,4), BN = tile columns
 };
-static_assert(kSplitGateTile == 20, "tile table");
+static_assert(kSplitGateTile == 20 && kSplitWinoTile == 21, "tile table");
 constexpr int kNumSplitTiles = sizeof(kSplitTiles) / sizeof(kSplitTiles[0]);
 
 }  // namespace
@@ -119,6 +120,10 @@ int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res)
 }
 
 void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, hipStream_t s) {
+  if (tile == kSplitWinoTile) {
+    launch_wino(mode, a, B, K, s);
+    return;
+  }
   TTS_REQUIRE((K == 2) == (a.ups > 0), 1, "conv1d(split): K == 2 is the ConvTranspose1d form (ups > 0)");
   TTS_REQUIRE(a.ups == 0 || ((a.ups & (a.ups - 1)) == 0 && a.Cout % a.ups == 0 && a.zmode == 0 && !a.res &&
                              !a.mask && a.Tout == a.Tin + 1 && a.pad == 1),

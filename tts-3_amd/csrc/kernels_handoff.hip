@@ -89,23 +89,31 @@ __global__ void __launch_bounds__(256) handoff_kernel(HandoffArgs a) {
 void launch_handoff(const HandoffArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.T_out, 256), a.C, B);
   hipLaunchKernelGGL(handoff_kernel, grid, dim3(256), 0, s, a);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
 // save_wav scaling: wav_norm = wav * (32767 / max(0.01, max|wav|)); astype(int16) (truncation).
 // Pass 1: per-utterance max|wav| (atomicMax on the fp32 bits, non-negative); pass 2: scale +
 // truncate.  len[b] (or n when len is NULL) bounds each utterance's samples.
+// Non-finite contract (numpy on x86, numpy_transforms.py:436-438, pinned by
+// tests/test_oracle_golden.py::test_wav_int16_nonfinite_contract):
+//  * np.max propagates NaN and Python's max(0.01, nan) returns 0.01, so one NaN sample makes the
+//    scale 32767 / 0.01: the max runs on the fp32 bits as unsigned integers (|NaN| sorts above inf);
+//  * astype(int16) converts through int32 (cvttss2si: NaN, +-inf and |v| >= 2^31 give INT_MIN)
+//    and keeps the low 16 bits, so those samples become 0 and other out-of-range ones wrap.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) wav_amax_kernel(const float* __restrict__ wav, int64_t n,
                                                        const int64_t* __restrict__ len, unsigned* __restrict__ amax) {
   const int b = blockIdx.y;
   const int64_t L = len ? (len[b] < n ? len[b] : n) : n;
   const float* w = wav + (size_t)b * n;
-  float m = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < L; i += (int64_t)gridDim.x * 256) m = fmaxf(m, fabsf(w[i]));
+  unsigned m = 0u;  // fp32 bits of |w|: unsigned order = float order, NaN above inf
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < L; i += (int64_t)gridDim.x * 256)
+    m = max(m, __float_as_uint(w[i]) & 0x7FFFFFFFu);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax + b, __float_as_uint(m));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(amax + b, m);
 }
 
 __global__ void __launch_bounds__(256) wav_int16_kernel(const float* __restrict__ wav, int64_t n,
@@ -113,12 +121,16 @@ __global__ void __launch_bounds__(256) wav_int16_kernel(const float* __restrict_
                                                         const unsigned* __restrict__ amax, int16_t* __restrict__ out) {
   const int b = blockIdx.y;
   const int64_t L = len ? (len[b] < n ? len[b] : n) : n;
-  const float mx = fmaxf(0.01f, __uint_as_float(amax[b]));
+  const float mx = fmaxf(0.01f, __uint_as_float(amax[b]));  // fmaxf(0.01, NaN) = 0.01, as max(0.01, nan)
   const float scale = 32767.f / mx;
   const float* w = wav + (size_t)b * n;
   int16_t* o = out + (size_t)b * n;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    o[i] = i < L ? (int16_t)(int)(w[i] * scale) : (int16_t)0;  // C cast truncates like astype
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = w[i] * scale;
+    // truncation toward zero like astype; NaN / inf / |v| >= 2^31 -> INT_MIN (x86 cvttss2si) -> 0
+    const int iv = (v >= -2147483648.f && v < 2147483648.f) ? (int)v : (int)0x80000000;
+    o[i] = i < L ? (int16_t)iv : (int16_t)0;
+  }
 }
 
 void launch_wav_int16(const float* wav, int B, int64_t n, const int64_t* len, unsigned* amax, int16_t* out,
@@ -127,7 +139,9 @@ void launch_wav_int16(const float* wav, int B, int64_t n, const int64_t* len, un
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
   dim3 grid(blocks, B);
   hipLaunchKernelGGL(wav_amax_kernel, grid, dim3(256), 0, s, wav, n, len, amax);
+  TTS_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(wav_int16_kernel, grid, dim3(256), 0, s, wav, n, len, amax, out);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace tts

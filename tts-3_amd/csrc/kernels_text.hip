@@ -43,6 +43,7 @@ void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, floa
                   int T, int num_chars, float scale, hipStream_t s) {
   dim3 grid(ceil_div(T, 64), B);
   hipLaunchKernelGGL(embed_kernel, grid, dim3(256), 0, s, tok, len, emb, x, mask, H, T, num_chars, scale);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
@@ -119,6 +120,7 @@ void launch_layernorm(const float* a, const float* r, const float* gamma, const 
   TTS_REQUIRE(C <= LN_S * LN_MAXV, 3, "LayerNorm: more than 768 channels");
   dim3 grid(ceil_div(T, LN_T), B);
   hipLaunchKernelGGL(layernorm_kernel, grid, dim3(256), 0, s, a, r, gamma, beta, mask, y, C, T, eps, relu ? 1 : 0);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
@@ -284,6 +286,7 @@ void launch_attention(const float* qkv, const float* mask, const float* ek, cons
   dim3 grid(ceil_div(T, ATT_QB), heads, B);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), lds, s, qkv, mask, W > 0 ? ek : nullptr,
                      W > 0 ? ev : nullptr, out, H, dk, T, W);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
@@ -320,6 +323,7 @@ __global__ void __launch_bounds__(256) durations_kernel(const float* __restrict_
 void launch_durations(const float* logw, const float* xm, float* w_ceil, int64_t* y_len, float* dur, int B, int T,
                       float length_scale, hipStream_t s) {
   hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, s, logw, xm, w_ceil, y_len, dur, T, length_scale);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
@@ -389,6 +393,7 @@ void launch_expand(const ExpandArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.T_x <= EXPAND_MAX_TX, 3, "expand: more than " + std::to_string(EXPAND_MAX_TX) + " tokens");
   dim3 grid(ceil_div(a.T_y, 256), B);
   hipLaunchKernelGGL(expand_kernel, grid, dim3(256), sizeof(float) * (size_t)a.T_x, s, a);
+  TTS_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace tts

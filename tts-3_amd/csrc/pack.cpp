@@ -69,12 +69,12 @@ static int split_pieces(int mode) { return mode == MATH_FP32_F16X3 ? 2 : (mode =
 
 // Split-mode A-operand fragments (conv1d_split_kernel), in floats (2 x 16-bit per float):
 //   out[mb][c16][k][piece][lane][j] = piece_p(w'[mb*32 + (lane&31)][c16*16 + 8*(lane>>5) + j][k])
-// plus 2 steps of slack for the prefetch.  w' = w for bf16x6, w * 2^-e for fp16 hi/lo with e
+// plus 4 steps of slack for the prefetch (up to 4 steps ahead).  w' = w for bf16x6, w * 2^-e for fp16 hi/lo with e
 // chosen so max|w'| lies in [2^13, 2^14) (exact; undone in the kernel epilogue).
 int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t) {
   const int64_t mblocks = (int64_t)ceil_div(Cout, t.BM) * (t.BM / 32);
   const int64_t groups = (int64_t)ceil_div(Cin, t.CK) * (t.CK / 16);
-  return (mblocks * groups * K + 2) * split_pieces(mode) * 64 * 4;
+  return (mblocks * groups * K + 4) * split_pieces(mode) * 64 * 4;
 }
 
 int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f) {
@@ -111,7 +111,7 @@ int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const 
           for (int lane = 0; lane < 64; ++lane)
             for (int j = 0; j < 8; ++j) out[o++] = pc[p][lane][j];
       }
-  for (int i = 0; i < 2 * NP * 64 * 8; ++i) out[o++] = 0;
+  for (int i = 0; i < 4 * NP * 64 * 8; ++i) out[o++] = 0;
   return e;
 }
 

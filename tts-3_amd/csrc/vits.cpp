@@ -65,6 +65,7 @@ void vits_flow_validate(const TtsVitsFlowCfg& c) {
 
 VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device) : cfg_(cfg), device_(device) {
   vits_flow_validate(cfg_);
+  amax_prepass_ = flow_amax_prepass();
   DeviceGuard g(device_);
   const auto shapes = vits_flow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -240,7 +241,7 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
     }
     const int fi = cfg_.num_flows - 1 - f;
     const int half = C / 2;
-    if (h3 && fi == 0)  // statistics of x0 (pre's input half); later flows: the previous post conv
+    if (h3 && (fi == 0 || amax_prepass_))  // statistics of x0 (pre's input half); later flows: the previous post conv
       run(prof, s, "vits_amax_x0", 0.0, 2.0 * P * half,
           [&] { launch_amax(y + Fl.in_off * T, (int64_t)half * T, B, slots(fi, 0), s, xbs); });
     // h = pre(x0) * mask  (networks.py:157)
@@ -269,7 +270,7 @@ void VitsFlow::reverse(const float* x, const float* mask, const float* g, int B,
     float* x1 = y + Fl.out_off * T;
     // the half it writes is the next flow's x0 (the flip alternates the halves): its statistics
     conv("vits_post", Fl.post, skip, 0, x1, mask, x1, xbs, nullptr, 0, true, slots(fi, 2 * L + 1),
-         f > 0 ? slots(fi + 1, 0) : nullptr);
+         f > 0 && !amax_prepass_ ? slots(fi + 1, 0) : nullptr);
   }
   if (odd) run(prof, s, "vits_flip", 0.0, 8.0 * P * C, [&] { launch_channel_flip(work, out, B, C, T, s); });
 }

@@ -47,6 +47,7 @@ class VitsFlow {
   float* arena_ = nullptr;
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;
+  bool amax_prepass_ = false;
 };
 
 }  // namespace tts

@@ -1,0 +1,481 @@
+// Winograd F(4,4) conv1d on the 16-bit split-precision MFMAs (gfx950).
+//
+// The MRF convs of HiFiGAN (hifigan_generator.py:93-98, kernel 7 and 11, dilation 1/3/5) are
+// cross-correlations y[t] = sum_k w[k] x[t - pad + d*k].  The taps are padded with zeros to 4*NCH
+// and cut into NCH chunks of 4; every chunk is a 4-tap correlation computed for 4 outputs at once
+// by the Toom-Cook/Winograd algorithm F(4,4) with the 7 points {0, 1, -1, 2, -2, 1/2, inf}:
+//
+//   y[t_i] = sum_c sum_p AT[i][p] * (U_c[p] . V_{tile+c}[p]),  t_i = tile base + d*i, i = 0..3
+//   U_c[p] = sum_k G[p][k] w[4c + k]         (weights, fp64 on the host, then fp32 -> split)
+//   V[p]   = sum_q BT[p][q] x[base + d*q]     (input, q = 0..6, fp32 in the staging)
+//
+// so one output costs 7*NCH/4 products per (co, ci) instead of K: 3.5 instead of 7 (k7) and 5.25
+// instead of 11 (k11).  Each point p is a dense [Cout x Cin] GEMM over the tiles; the chunk
+// shift c moves the tile by d*c columns, exactly like a tap shift of the direct kernel
+// (split_kernel.hpp), so the main loop is that kernel's with (point, chunk) steps and one
+// accumulator per point.  The transforms only add, subtract and scale by small integers /
+// powers of two in fp32; BT is integer (rows scaled to coprime integers, the factors moved into
+// G), AT holds 1, +-2^k.  Measured error growth over the direct f16x3 conv: ~3x rel-RMS on
+// random 128-channel convs (both ~1e-6, the fp32 tolerance is 1e-5).
+//
+// Columns: GEMM column n = jj*D + rho (rho = n mod D) is the tile of outputs
+// t0 + rho + D*(4*jj + i); tile jj + c of the same residue is column n + c*D.  The staging
+// computes V for XROWS = 32*TN + (NCH-1)*D columns per 16-channel chunk into LDS
+// ([buffer][point][row][piece][16 ch]); the transforms of chunk c+1 run as jobs placed between
+// the MFMA steps of chunk c (one wave per SIMD: nothing else hides that VALU work).
+#pragma once
+
+#include "split_device.hpp"
+
+namespace tts {
+
+#ifndef WINO_ABLATE
+#define WINO_ABLATE 0  // ablation builds (timing only, wrong results): 1 no x loads, 2 no transform jobs, 4 no A stream,
+                       // 8 no MFMA, 16 no epilogue
+#endif
+
+constexpr int kWinoPoints = 7;
+constexpr int wino_chunks(int K) { return (K + 3) / 4; }
+// G[p][k] = gc[p] * ga[p]^k (k = 0..3); p = 6 (inf) only has k = 3.
+constexpr double kWinoGc[7] = {0.25, 1.0 / 6, 1.0 / 18, 1.0 / 72, 1.0 / 120, 32.0 / 45, 0.5};
+constexpr double kWinoGa[7] = {0.0, 1.0, -1.0, 2.0, -2.0, 0.5, 0.0};
+constexpr int kWinoBtShift = 5;  // max row sum of |BT| = 30 < 2^5: scale the input by 2^-(e+5)
+
+// V[p] = BT[p] . v for one channel (20 fp32 ops):
+//   BT = [[4,-8,-5,10,1,-2,0], [0,-4,4,9,-1,-2,0], [0,-4,12,-7,-3,2,0], [0,2,-3,-4,3,2,0],
+//         [0,2,-5,0,5,-2,0], [0,4,0,-5,0,1,0], [0,-4,8,5,-10,-1,2]]
+__host__ __device__ inline void wino_bt(const float (&v)[7], float (&t)[7]) {
+  float p[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) p[k] = fmaf(-2.f, v[k + 1], v[k]);  // p_k = v_k - 2 v_{k+1}
+  const float A = fmaf(-4.f, p[1], p[3]);
+  const float Bq = fmaf(-4.f, p[2], p[4]);
+  const float Cq = p[1] - p[3];
+  const float Dq = p[2] - p[4];
+  t[0] = fmaf(4.f, p[0], fmaf(-5.f, p[2], p[4]));
+  t[1] = A + Bq;
+  t[2] = A - Bq;
+  t[3] = fmaf(2.f, Cq, Dq);
+  t[4] = fmaf(2.f, Cq, -Dq);
+  t[5] = fmaf(4.f, v[1], fmaf(-5.f, v[3], v[5]));
+  t[6] = fmaf(5.f, p[3], fmaf(-4.f, p[1], -p[5]));
+}
+
+// y_i = AT[i] . m, AT = [[1,1,1,1,1,1,0], [0,1,-1,2,-2,1/2,0], [0,1,1,4,4,1/4,0], [0,1,-1,8,-8,1/8,1]]
+__host__ __device__ inline void wino_at(const float (&m)[7], float (&y)[4]) {
+  const float a = m[1] + m[2], b = m[1] - m[2], c = m[3] + m[4], e = m[3] - m[4];
+  y[0] = ((m[0] + a) + c) + m[5];
+  y[1] = fmaf(2.f, e, b) + 0.5f * m[5];
+  y[2] = fmaf(4.f, c, a) + 0.25f * m[5];
+  y[3] = (fmaf(8.f, e, b) + 0.125f * m[5]) + m[6];
+}
+
+// two values -> NP 32-bit words (piece p of value 0 in the low half, of value 1 in the high half)
+template <class S>
+__device__ __forceinline__ void split_pair(float x0, float x1, unsigned (&w)[S::NP]) {
+  if constexpr (S::SCALED) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const f2 v = {x0, x1};
+    const h2 h = __builtin_convertvector(v, h2);  // v_cvt_pk_f16_f32 (round to nearest even)
+    const f2 hb = __builtin_convertvector(h, f2);
+    const f2 r = {x0 - hb[0], x1 - hb[1]};
+    w[0] = __builtin_bit_cast(unsigned, h);
+    w[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, h2));
+  } else {
+    unsigned short a[S::NP], b[S::NP];
+    S::split(x0, a);
+    S::split(x1, b);
+#pragma unroll
+    for (int p = 0; p < S::NP; ++p) w[p] = (unsigned)a[p] | ((unsigned)b[p] << 16);
+  }
+}
+
+template <class S, int NCH, int D, int TN>
+struct WinoCfg {
+  static constexpr int NPT = kWinoPoints;
+  static constexpr int NS = NPT * NCH;                 // steps per 16-channel chunk
+  static constexpr int BNT = 32 * TN;                  // GEMM columns (tiles) per workgroup
+  static constexpr int J = BNT / D;                    // tiles per residue class
+  static constexpr int TW = 4 * D * J;                 // output samples per workgroup
+  static constexpr int XROWS = BNT + (NCH - 1) * D;    // staged columns (halo of the chunk shifts)
+  static constexpr int PLANE = XROWS * S::ROWB;        // bytes per point plane
+  static constexpr int XSZB = NPT * PLANE;             // bytes per buffer
+  static constexpr int UNITS = XROWS * 4;              // staging units (column, channel quad)
+  static constexpr int UPT = (UNITS + 255) / 256;
+  static constexpr int NJOB = 2 * UPT;                 // (unit, channel pair) jobs per thread
+  static constexpr int JS0 = NS * 3 / 7;               // first step carrying a job
+  static constexpr int JSTEP = (NS - JS0) / NJOB > 0 ? (NS - JS0) / NJOB : 1;
+  static_assert(J >= 1, "tile narrower than the dilation");
+  static constexpr int PITCH = TW <= 128 ? 128 : 256;  // epilogue transpose: samples per LDS row
+  static_assert(TW <= 256 && 2 * XSZB >= 4 * 16 * PITCH * 4, "epilogue transpose: 16 rows per wave in the staging LDS");
+};
+
+// Epilogue: y = AT . (acc * scale) for the 4 outputs of every (row, tile), then
+//   v = act_out(y + bias [+ cvec]) [+ res];  zmode 0: y = v, 1: z = v, 2: z += v, 3: z = (z + v) / zdiv
+// stored as 16-byte vectors of 4 consecutive samples (the output rows are contiguous in time):
+// * D = 1: a lane's 4 outputs ARE consecutive samples: straight from the registers;
+// * D > 1: they are D apart, so each wave transposes its rows through LDS (16 rows x 256 samples
+//   per pass, two passes; the 2-way bank conflicts of the scattered writes are free on ds_write_b32)
+//   and then stores one row per instruction.
+// Residual / z values are gathered before the stores of the same vector (res may alias y).
+template <bool RES, int ZM, bool H3>
+__device__ __forceinline__ f32x4 wino_finish(f32x4 y, float bias, float oslope, float zdiv, const rsrc_t& rres,
+                                              const rsrc_t& rz, unsigned voff, bool full, int nvalid, float& vm) {
+  f32x4 rv = {}, zv = {};
+  if (full) {
+    if (RES) rv = bload4(rres, voff, 0u);
+    if (ZM >= 2) zv = bload4(rz, voff, 0u);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned o = j < nvalid ? voff + 4u * j : OOB_OFF;
+      if (RES) rv[j] = bload(rres, o, 0u);
+      if (ZM >= 2) zv[j] = bload(rz, o, 0u);
+    }
+  }
+  f32x4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x = lrelu2(y[j] + bias, oslope);
+    if (RES) x = x + rv[j];
+    if (ZM == 2) x = zv[j] + x;
+    if (ZM == 3) x = (zv[j] + x) / zdiv;
+    if (H3 && j < nvalid) vm = fmaxf(vm, fabsf(x));
+    v[j] = x;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void wino_store(const rsrc_t& rout, f32x4 v, unsigned voff, bool full, int nvalid) {
+  if (full) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)voff, 0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bstore(rout, v[j], j < nvalid ? voff + 4u * j : OOB_OFF, 0u);
+  }
+}
+
+template <class C, int TN, bool H3, bool RES, int ZM>
+__device__ __forceinline__ void wino_epilogue(const Conv1dArgs& a, const f32x16 (&acc)[kWinoPoints][TN], float sc,
+                                              int b, int t0, int cobase, int lane, unsigned char* lds) {
+  constexpr int D = C::TW / (4 * C::J);
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int Cout = a.Cout;
+  const int Tout = a.Tout;
+  const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;
+  const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
+  const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
+  const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
+  const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
+  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
+  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
+                               a.cvec ? (unsigned)Cout * 4u : 0u);
+  const float oslope = a.out_slope;
+  const float zdiv = a.zdiv;
+  float vmax = 0.f;
+  auto yval = [&](int n, int r, float (&yy)[4]) {
+    float m[kWinoPoints];
+#pragma unroll
+    for (int p = 0; p < kWinoPoints; ++p) m[p] = acc[p][n][r] * sc;
+    wino_at(m, yy);
+  };
+  if constexpr (D == 1) {
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
+      bv[r] = bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
+    }
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int t = t0 + 4 * (n * 32 + l32);  // samples t .. t+3 of the lane's tile
+      const int nvalid = Tout - t < 4 ? (Tout - t > 0 ? Tout - t : 0) : 4;
+      const bool full = nvalid == 4 && (Tout & 3) == 0;  // 16-byte aligned rows
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
+        const unsigned voff = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+        float yy[4];
+        yval(n, r, yy);
+        const f32x4 y = {yy[0], yy[1], yy[2], yy[3]};
+        const f32x4 v = wino_finish<RES, ZM, H3>(y, bv[r], oslope, zdiv, rres, rz, voff, full, nvalid, vmax);
+        wino_store(rout, v, voff, full, nvalid);
+      }
+    }
+  } else {
+    // per wave: 16 rows x PITCH samples of fp32 per pass; the read phase covers 256 / PITCH rows
+    // per instruction (lane -> row sub-index lane / (PITCH / 4), samples tl .. tl+3)
+    constexpr int PITCH = C::PITCH, LPR = PITCH / 4, RPI = 64 / LPR;
+    float* tile = reinterpret_cast<float*>(lds) + (threadIdx.x >> 6) * (16 * PITCH);
+    const int tl = 4 * (lane % LPR);
+    const int t = t0 + tl;
+    const int lim = (C::TW < Tout - t0 ? C::TW : Tout - t0) - tl;
+    const int nvalid = lim < 4 ? (lim > 0 ? lim : 0) : 4;
+    const bool full = nvalid == 4 && (Tout & 3) == 0;  // 16-byte aligned rows (TW, t0 multiples of 4)
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+      __syncthreads();  // the staging buffers / the previous pass's rows are no longer read
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int nn = n * 32 + l32;
+        const int jj = nn / D, rho = nn - (nn / D) * D;
+#pragma unroll
+        for (int r = 8 * ps; r < 8 * ps + 8; ++r) {
+          const int rl = (r & 3) + 8 * ((r >> 2) - 2 * ps) + 4 * half;
+          float yy[4];
+          yval(n, r, yy);
+          if (jj < C::J) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tile[rl * PITCH + rho + D * (4 * jj + i)] = yy[i];
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < 16; rr += RPI) {
+        const int rl = rr + lane / LPR;
+        const int co = cobase + 16 * ps + rl;
+        const float bias = bload(rbias, (unsigned)co * 4u, 0u) + bload(rcv, (unsigned)co * 4u, 0u);
+        const unsigned voff = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+        const f32x4 y = *reinterpret_cast<const f32x4*>(tile + rl * PITCH + tl);
+        const f32x4 v = wino_finish<RES, ZM, H3>(y, bias, oslope, zdiv, rres, rz, voff, full, nvalid, vmax);
+        wino_store(rout, v, voff, full, nvalid);
+      }
+    }
+  }
+  if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+}
+
+// TN = 1: 112 accumulator registers, two workgroups per CU (one hides the other's input-load
+// latency behind its MFMAs); TN = 2: 224, one workgroup per CU
+template <class S, int NCH, int D, int TN, int PD, bool LRELU>
+__global__ __launch_bounds__(256, TN == 1 ? 2 : 1) void conv1d_wino_kernel(Conv1dArgs a) {
+  using C = WinoCfg<S, NCH, D, TN>;
+  constexpr int NP = S::NP;
+  constexpr int NPT = C::NPT;
+  constexpr bool H3 = S::SCALED;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wm = tid >> 6;  // row block: 4 waves x 32 output channels
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int b = blockIdx.z;
+  const int mt = blockIdx.y;
+  const int t0 = blockIdx.x * C::TW;
+  const int Tin = a.Tin;
+  const int Cin = a.Cin;
+  const int nc = a.n_chunks;
+  const int ex = H3 ? amax_exp(a.amax_in, b) + kWinoBtShift : 0;
+  const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;  // exact power of two
+  const float slope = a.in_slope;
+
+  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  const unsigned chb = (unsigned)Tin * 4u;
+
+  // staging units: unit u -> column row = u >> 2, channel quad q = u & 3; its 7 input times
+  // t0 - pad + rho' + D*(4*jj' + k), k = 0..6 (zero outside [0, Tin): OOB offsets)
+  unsigned uvoff[C::UPT][7];
+  int ulds[C::UPT];
+#pragma unroll
+  for (int i = 0; i < C::UPT; ++i) {
+    const int u = tid + i * 256;
+    const int row = u >> 2;
+    const int q = u & 3;
+    const int jj = row / D, rho = row - (row / D) * D;
+    const int tb = t0 - a.pad + rho + 4 * D * jj;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int ts = tb + D * k;
+      uvoff[i][k] = (u < C::UNITS && ts >= 0 && ts < Tin) ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+    }
+    ulds[i] = u < C::UNITS ? row * S::ROWB + 8 * q : -1;
+  }
+
+  float xr[C::UPT][4][7];
+  auto load_x = [&](int c) {
+    const int c0 = c * 16;
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
+#pragma unroll
+    for (int i = 0; i < C::UPT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) xr[i][j][k] = bload(rx, uvoff[i][k] + (unsigned)j * chb, 0u);
+  };
+  // job (i, jp): channels 2jp, 2jp+1 of unit i -> 7 points x NP pieces, one 32-bit LDS word each
+  auto stage_job = [&](int buf, int i, int jp) {
+    if (ulds[i] < 0) return;
+    float t[2][7];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        float x = xr[i][2 * jp + h][k];
+        if (LRELU) x = lrelu2(x, slope);
+        v[k] = H3 ? x * xscale : x;
+      }
+      wino_bt(v, t[h]);
+    }
+    unsigned char* base = smem + buf * C::XSZB + ulds[i] + 4 * jp;
+#pragma unroll
+    for (int p = 0; p < NPT; ++p) {
+      unsigned w[NP];
+      split_pair<S>(t[0][p], t[1][p], w);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) *reinterpret_cast<unsigned*>(base + p * C::PLANE + 32 * q) = w[q];
+    }
+  };
+
+  // A stream (one 32-row block per wave): fragment (step s, piece q) at (s*NP + q)*1 KiB
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+  const int mb = mt * 4 + wmu;
+  const rsrc_t ra = make_rsrc(a.w + ((size_t)mb * nc * C::NS) * (NP * 256), 0xFFFFFFFFu);
+  const unsigned avoff = (unsigned)lane * 16u;
+
+  f32x16 acc[NPT][TN];
+#pragma unroll
+  for (int p = 0; p < NPT; ++p)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[p][n] = f32x16{};
+
+  f32x4 ar[PD + 1][NP], bcur[TN][NP], bnext[TN][NP];
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+#pragma unroll
+    for (int q = 0; q < NP; ++q) ar[p][q] = bload4(ra, avoff, (unsigned)(p * NP + q) * 1024u);
+
+  auto read_b = [&](const unsigned char* xl, int s, f32x4 (*dst)[NP]) {
+    const int p = s % NPT, c = s / NPT;
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const unsigned char* ptr = xl + p * C::PLANE + (n * 32 + l32 + c * D) * S::ROWB + 16 * half;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(ptr + 32 * q);
+    }
+  };
+
+  load_x(0);
+#pragma unroll
+  for (int i = 0; i < C::UPT; ++i)
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) stage_job(0, i, jp);
+  __syncthreads();
+
+  for (int c = 0; c < nc; ++c) {
+    const int buf = c & 1;
+    const unsigned char* xl = smem + buf * C::XSZB;
+    const bool more = c + 1 < nc;
+    if ((WINO_ABLATE & 1) == 0 && more) load_x(c + 1);
+    read_b(xl, 0, bcur);
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      const int sg = c * C::NS + s;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ar[PD][q] = (WINO_ABLATE & 4) ? ar[0][q] : bload4(ra, avoff, (unsigned)((sg + PD) * NP + q) * 1024u);
+      if (s + 1 < C::NS) read_b(xl, s + 1, bnext);
+      __builtin_amdgcn_sched_barrier(0);
+      const int p = s % NPT;
+#pragma unroll
+      for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+        for (int n = 0; n < TN; ++n) {
+          if (WINO_ABLATE & 8) acc[p][n][e] += ar[0][S::PA[e]][0] * bcur[n][S::PB[e]][0];
+          else acc[p][n] = S::mfma(ar[0][S::PA[e]], bcur[n][S::PB[e]], acc[p][n]);
+        }
+#pragma unroll
+      for (int pp = 0; pp < PD; ++pp)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[pp][q] = ar[pp + 1][q];
+      if (s + 1 < C::NS) {
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+      }
+      // transform jobs of the next chunk between this chunk's MFMA steps
+#pragma unroll
+      for (int jb = 0; jb < C::NJOB; ++jb) {
+        const int js = C::JS0 + jb * C::JSTEP;
+        if ((WINO_ABLATE & 2) == 0 && more && s == (js < C::NS ? js : C::NS - 1)) stage_job(buf ^ 1, jb >> 1, jb & 1);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue (one uniform dispatch on residual / MRF mode, no per-element branches) ----
+  const float sc = H3 ? ldexpf(1.f, ex + a.w_exp) : 1.f;  // undo both scalings (exact)
+  const int zm = a.zmode <= 1 ? 0 : a.zmode;
+  if (WINO_ABLATE & 16) {
+    float sum = 0.f;
+#pragma unroll
+    for (int p = 0; p < NPT; ++p)
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += acc[p][n][r];
+    if (sum == 1234.5f) a.y[threadIdx.x] = sum;
+    return;
+  }
+  if (a.res) {
+    if (zm == 0) wino_epilogue<C, TN, H3, true, 0>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+    else if (zm == 2) wino_epilogue<C, TN, H3, true, 2>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+    else wino_epilogue<C, TN, H3, true, 3>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+  } else {
+    if (zm == 0) wino_epilogue<C, TN, H3, false, 0>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+    else if (zm == 2) wino_epilogue<C, TN, H3, false, 2>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+    else wino_epilogue<C, TN, H3, false, 3>(a, acc, sc, b, t0, mt * 128 + wm * 32, lane, smem);
+  }
+}
+
+namespace wino_detail {
+#ifndef WINO_PD
+#define WINO_PD 3
+#endif
+#ifndef WINO_TN
+#define WINO_TN 1
+#endif
+template <class S, int NCH, int D>
+void launch_wino_d(const Conv1dArgs& a, int B, hipStream_t s) {
+  constexpr int TN = WINO_TN, PD = WINO_PD;
+  using C = WinoCfg<S, NCH, D, TN>;
+  const dim3 grid(ceil_div(a.Tout, C::TW), ceil_div(a.Cout, 128), B);
+  // the identity input activation (convs2, dilation 1) skips the leaky_relu; other dilations
+  // only occur on convs1 (slope 0.1), so only these two forms are instantiated
+  if constexpr (D == 1) {
+    if (a.in_slope == 1.f) {
+      hipLaunchKernelGGL((conv1d_wino_kernel<S, NCH, D, TN, PD, false>), grid, dim3(256), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv1d_wino_kernel<S, NCH, D, TN, PD, true>), grid, dim3(256), 0, s, a);
+}
+
+template <class S, int NCH>
+void launch_wino_k(const Conv1dArgs& a, int B, hipStream_t s) {
+  switch (a.dil) {
+    case 1: launch_wino_d<S, NCH, 1>(a, B, s); break;
+    case 3: launch_wino_d<S, NCH, 3>(a, B, s); break;
+    case 5: launch_wino_d<S, NCH, 5>(a, B, s); break;
+    default: throw Error(3, "conv1d(winograd): dilation must be 1, 3 or 5");
+  }
+}
+
+template <class S>
+void launch_wino_s(const Conv1dArgs& a, int B, int K, hipStream_t s) {
+  TTS_REQUIRE(a.mask == nullptr && a.ups == 0 && a.gate == 0 && a.rep_pad == 0 && a.Tin == a.Tout &&
+                  a.pad == a.dil * (K - 1) / 2,
+              1, "conv1d(winograd): unsupported arguments");
+  switch (K) {
+    case 7: launch_wino_k<S, 2>(a, B, s); break;
+    case 11: launch_wino_k<S, 3>(a, B, s); break;
+    default: throw Error(3, "conv1d(winograd): kernel size must be 7 or 11");
+  }
+}
+}  // namespace wino_detail
+
+}  // namespace tts
