@@ -93,6 +93,14 @@ WINO_CASES = [
     (2, 128, 128, 9, 7, 5, 0.1, 0.1, True, 1),       # shorter than the halo
     (3, 144, 256, 263, 11, 3, 0.1, 1.0, True, 0),    # Cin != Cout, 9 channel chunks
     (1, 128, 384, 1283, 11, 1, 0.1, 0.1, False, 0),  # 3 row blocks, ragged last workgroup
+    # T % 4 == 0: the 8-wave form (LDS-DMA input windows)
+    (2, 128, 128, 1028, 11, 5, 0.1, 0.1, False, 0),
+    (1, 128, 128, 2048, 11, 3, 1.0, 1.0, True, 2),
+    (2, 256, 256, 516, 7, 1, 1.0, 1.0, True, 3),
+    (1, 128, 128, 8, 7, 5, 0.1, 0.1, True, 1),      # shorter than the halo
+    (3, 144, 128, 252, 11, 1, 0.1, 0.1, False, 0),  # 9 channel chunks (odd)
+    (1, 16, 128, 64, 11, 1, 0.1, 0.1, False, 0),    # one channel chunk
+    (2, 32, 256, 300, 7, 3, 0.1, 1.0, True, 0),     # two channel chunks, 2 row blocks
 ]
 
 
@@ -289,7 +297,7 @@ def test_split_modes_accuracy_not_worse_than_fp32(cuda_device, monkeypatch):
     F(4,4) form of the >= 128-channel MRF convs (f16x3 default) stays within 4x of it."""
     name, meta, arr = [h for h in HIFI if h[0] == "hifigan_v1_b2_t32"][0]
     errs = {}
-    for mode, wino in (("fp32", "0"), ("fp32x6", "0"), ("f16x3", "0"), ("f16x3_wino", "all")):
+    for mode, wino in (("fp32", "0"), ("fp32x6", "0"), ("f16x3", "0"), ("f16x3_wino", "1")):
         monkeypatch.setenv("TTS_MI355X_WINO", wino)
         g = build(meta["config"], meta["seed"], cuda_device, mode.split("_")[0])
         out = g.inference(torch.from_numpy(arr["mel"]).to(cuda_device)).cpu().numpy()
@@ -310,7 +318,7 @@ def test_winograd_generator_matches_direct(cuda_device, monkeypatch):
     mel = synthetic.mel(2, 61, seed=5)
     ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
     outs = []
-    for wino in ("all", "1", "0"):  # every supported MRF conv / the default selection / none
+    for wino in ("1", "0"):  # Winograd for every supported MRF conv / none
         monkeypatch.setenv("TTS_MI355X_WINO", wino)
         g = HifiganGenerator(**V1, math_mode="f16x3")
         g.remove_weight_norm()
@@ -318,4 +326,4 @@ def test_winograd_generator_matches_direct(cuda_device, monkeypatch):
         g = g.to(cuda_device)
         outs.append(g.inference(mel.to(cuda_device)).cpu())
         assert_close_fp32(outs[-1], ref, f"wino={wino}")
-    assert max_abs(outs[0].numpy(), outs[2].numpy()) < 2e-5 and max_abs(outs[1].numpy(), outs[2].numpy()) < 2e-5
+    assert max_abs(outs[0].numpy(), outs[1].numpy()) < 2e-5

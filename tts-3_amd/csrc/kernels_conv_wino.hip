@@ -1,10 +1,9 @@
 // Winograd F(4,4) conv1d instances (wino_kernel.hpp) and the weight transform (host).
 #include <cmath>
 #include <cstdlib>
-#include <string>
 #include <vector>
 
-#include "wino_kernel.hpp"
+#include "wino8_kernel.hpp"
 
 namespace tts {
 
@@ -19,10 +18,7 @@ bool wino_enabled() {
   const char* e = std::getenv("TTS_MI355X_WINO");
   return !(e && e[0] == '0');
 }
-bool wino_all() {
-  const char* e = std::getenv("TTS_MI355X_WINO");
-  return e && std::string(e) == "all";
-}
+
 
 // U_c[p][co][ci] = gc[p] * sum_k ga[p]^k w[co][ci][4c + k]  (fp64, taps >= K are zero), laid out as
 // the 7*NCH "taps" s = c*7 + p of an ordinary split-mode conv weight, then packed by
@@ -53,7 +49,14 @@ void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
   TTS_REQUIRE(wino_supported(mode, a.Cout, a.Cin, K, a.dil), 3, "conv1d(winograd): unsupported configuration");
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
-  wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
+  // the 8-wave form needs 16-byte aligned input rows (every HiFiGAN MRF conv at >= 128 channels:
+  // T = 8 * (T_mel + 2 pad) and more); TTS_MI355X_WINO8=0 keeps the 4-wave form (A/B runs)
+  static const bool w8 = [] {
+    const char* e = std::getenv("TTS_MI355X_WINO8");
+    return !(e && e[0] == '0');
+  }();
+  if (w8 && a.Tin % 4 == 0) wino8_detail::launch_s<SchemeH3>(a, B, K, s);
+  else wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

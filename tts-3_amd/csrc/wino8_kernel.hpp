@@ -1,0 +1,425 @@
+// Winograd F(4,4) conv1d, 8-wave point-split form (gfx950).  Same arithmetic as
+// conv1d_wino_kernel (wino_kernel.hpp: transforms, split, packed weights), different schedule:
+//
+// * 512 threads, two waves per SIMD.  Waves w and w+4 compute the same 32 output channels x 64
+//   tile columns; wave w accumulates points 0-3, wave w+4 points 4-6 (128 accumulator registers
+//   each instead of 224 for all seven), so the workgroup keeps two waves on every SIMD and one
+//   wave's stalls (input loads, transform VALU, barriers) overlap the other's MFMAs.
+// * The input window of a 16-channel chunk reaches LDS by LDS-DMA (buffer_load_dwordx4 ... lds),
+//   two chunks ahead, issued by waves 4-7 only: vector-memory counters retire in order, so the
+//   wave that issues an HBM load stalls at its next weight-prefetch wait until the load lands;
+//   waves 0-3, which carry 4/7 of the MFMAs, never issue one and keep the matrix pipe busy.
+// * The transform of chunk c+1 (raw fp32 window in LDS -> 7 split point planes) is spread evenly
+//   over all eight waves (one channel quad of one tile column per lane, four channel pieces
+//   placed between the MFMA steps of chunk c).
+// * Barriers are bare s_barrier with an explicit lgkmcnt wait: __syncthreads' fence would also
+//   drain the DMA and weight loads in flight.
+// * Epilogue: the two waves of a pair swap their partial point sums through LDS (each finishes
+//   one 32-column block), then store 16-byte vectors of 4 consecutive samples (dilation 1) or
+//   transpose their rows through LDS first (dilation 3, 5), as wino_kernel.hpp.
+#pragma once
+
+#include <type_traits>
+
+#include "wino_kernel.hpp"
+
+namespace tts {
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <class S, int K, int D>
+struct Wino8Cfg {
+  static constexpr int NCH = wino_chunks(K);
+  static constexpr int NS = kWinoPoints * NCH;       // packed steps per 16-channel chunk (c*7 + p)
+  static constexpr int PAD = D * (K - 1) / 2;
+  static constexpr int BNT = 64;                     // tile columns per workgroup (2 x 32)
+  static constexpr int J = BNT / D;                  // tiles per residue class
+  static constexpr int TW = 4 * D * J;               // output samples per workgroup
+  static constexpr int XROWS = BNT + (NCH - 1) * D;  // transformed columns (halo of the chunk shifts)
+  static constexpr int PLANE = XROWS * S::ROWB;
+  static constexpr int TSZ = kWinoPoints * PLANE;    // bytes of one transformed buffer
+  // raw window: times t0 - PAD - ROFF ... (16-byte aligned start; t0 is a multiple of 4)
+  static constexpr int ROFF = (4 - PAD % 4) % 4;
+  static constexpr int RSPAN = (XROWS - 1) % D + 4 * D * ((XROWS - 1) / D) + 6 * D + ROFF + 1;
+  static constexpr int RSPAN4 = (RSPAN + 3) / 4 * 4;
+  static constexpr int RPITCH = RSPAN4 % 8 == 4 ? RSPAN4 : RSPAN4 + 4;  // 4*RPITCH = 16 mod 32 banks
+  static constexpr int RF4 = (16 * RPITCH / 4 + 63) / 64 * 64;          // float4s per raw buffer (DMA rows of 64)
+  static constexpr int RSZ = RF4 * 16;
+  static constexpr int NDMA = RF4 / 64;              // DMA instructions per chunk (waves 4-7)
+  static constexpr int UNITS = XROWS * 4;            // (column, channel quad)
+  static constexpr int UPW = (UNITS + 7) / 8;        // units per wave
+  static constexpr int PITCH = 256;                  // epilogue transpose row (samples)
+  static_assert(UPW <= 64 && UNITS <= 256 + 64, "one transform round per wave");
+  static_assert(TW <= PITCH, "");
+  static_assert(2 * TSZ >= 4 * 16 * PITCH * 4 && 2 * TSZ >= 8 * 8 * 4 * 64 * 4, "epilogue LDS (transformed buffers)");
+};
+
+template <class S, int K, int D, bool LRELU>
+__global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
+  using C = Wino8Cfg<S, K, D>;
+  constexpr int NP = S::NP;
+  constexpr int NCH = C::NCH;
+  constexpr bool H3 = S::SCALED;
+#ifndef WINO8_PD
+#define WINO8_PD 2
+#endif
+  constexpr int PD = WINO8_PD;
+  __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
+  __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3;   // 32-row block
+  const int grp = wave >> 2;  // 0: points 0-3 (+ no loads), 1: points 4-6 (+ the input DMA)
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int b = blockIdx.z;
+  const int mt = blockIdx.y;
+  const int t0 = blockIdx.x * C::TW;
+  const int Tin = a.Tin;
+  const int Cin = a.Cin;
+  const int nc = a.n_chunks;
+  const int ex = H3 ? amax_exp(a.amax_in, b) + kWinoBtShift : 0;
+  const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;
+  const float slope = a.in_slope;
+  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
+  const unsigned chb = (unsigned)Tin * 4u;
+
+  // ---- input DMA (waves 4-7): raw[ch][RPITCH] fp32, window start ta = t0 - PAD - ROFF ----
+  const int ta = t0 - C::PAD - C::ROFF;
+  auto dma = [&](int c, int rb) {
+    const int c0 = c * 16;
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
+    for (int i = wm; i < C::NDMA; i += 4) {  // wave-uniform
+      const int f = i * 64 + lane;
+      const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
+      const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
+    }
+  };
+
+  // ---- transform jobs: unit (column row, channel quad q) ----
+#ifndef WINO8_DENSE
+#define WINO8_DENSE 1
+#endif
+  // dense: waves 4-7 (fewer MFMAs) take units 0-255 with every lane, wave 3 the rest; else every
+  // wave takes UPW units (balanced, but only UPW of its 64 lanes active)
+  const int u = WINO8_DENSE ? (grp == 1 ? (wave - 4) * 64 + lane : (wave == 3 ? 256 + lane : C::UNITS))
+                            : wave * C::UPW + lane;
+  const bool uok = (WINO8_DENSE || lane < C::UPW) && u < C::UNITS;
+  const int urow = u >> 2, uq = u & 3;
+  const int ujj = urow / D, urho = urow - (urow / D) * D;
+  const int uri = urho + 4 * D * ujj + C::ROFF;  // raw index of the column's first input
+  float tkeep[7];
+  // piece j: channel 4q + j; pairs are written after channels 1 and 3
+  auto job_piece = [&](int rb, int tb, int j) {
+    if (!uok) return;
+    const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + j) * C::RPITCH + uri;
+    float v[7], t[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      float x = raw[D * k];
+      if (LRELU) x = lrelu2(x, slope);
+      v[k] = H3 ? x * xscale : x;
+    }
+    wino_bt(v, t);
+    if ((j & 1) == 0) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) tkeep[k] = t[k];
+      return;
+    }
+    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 8 * uq + 4 * (j >> 1);
+#pragma unroll
+    for (int p = 0; p < kWinoPoints; ++p) {
+      unsigned w[NP];
+      split_pair<S>(tkeep[p], t[p], w);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) *reinterpret_cast<unsigned*>(base + p * C::PLANE + 32 * q) = w[q];
+    }
+  };
+
+  // ---- weights: this wave's 32-row block, packed steps (chunk, c*7 + p) ----
+  const int mb = mt * 4 + wm;
+  const rsrc_t ra = make_rsrc(a.w + ((size_t)mb * nc * C::NS) * (NP * 256), 0xFFFFFFFFu);
+  const unsigned avoff = (unsigned)lane * 16u;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = f32x16{};
+
+  // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0
+  if (grp == 1) {
+    dma(0, 0);
+    if (nc > 1) dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  lds_sync();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) job_piece(0, 0, j);
+  lds_sync();
+
+  // the chunk loop of one point group (NPG points starting at P0); both groups run it with the
+  // same barrier sequence
+  auto run = [&](auto npg_tag, auto p0_tag) {
+    constexpr int NPG = decltype(npg_tag)::value;
+    constexpr int P0 = decltype(p0_tag)::value;
+    constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
+    auto aoff = [&](int ck, int v) {  // byte soffset of virtual step v of chunk ck (v may run past NV)
+      const int ck2 = ck + v / NV, v2 = v % NV;
+      // prefetches past the last chunk (never used) re-read step 0 instead of running off the array
+      return ck2 < nc ? (unsigned)((ck2 * C::NS + (v2 / NPG) * 7 + P0 + v2 % NPG) * NP) * 1024u : 0u;
+    };
+    f32x4 ar[PD + 1][NP], bcur[2][NP], bnext[2][NP];
+#pragma unroll
+    for (int v = 0; v < PD; ++v)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ar[v][q] = bload4(ra, avoff, aoff(0, v) + (unsigned)q * 1024u);
+    auto read_b = [&](const unsigned char* tl, int v, f32x4 (*dst)[NP]) {
+      const int p = P0 + v % NPG, c = v / NPG;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const unsigned char* ptr = tl + p * C::PLANE + (n * 32 + l32 + c * D) * S::ROWB + 16 * half;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(ptr + 32 * q);
+      }
+    };
+    for (int ck = 0; ck < nc; ++ck) {
+      const int tb = ck & 1;
+      const unsigned char* tl = tsm + tb * C::TSZ;
+      const bool more = ck + 1 < nc;
+      if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc) dma(ck + 2, tb);  // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed)
+      read_b(tl, 0, bcur);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[PD][q] = bload4(ra, avoff, aoff(ck, v + PD) + (unsigned)q * 1024u);
+        if (v + 1 < NV) read_b(tl, v + 1, bnext);
+        __builtin_amdgcn_sched_barrier(0);
+        const int p = v % NPG;
+#pragma unroll
+        for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            if (WINO_ABLATE & 8) acc[p][n][e] += ar[0][S::PA[e]][0] * bcur[n][S::PB[e]][0];
+            else acc[p][n] = S::mfma(ar[0][S::PA[e]], bcur[n][S::PB[e]], acc[p][n]);
+          }
+#pragma unroll
+        for (int pp = 0; pp < PD; ++pp)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) ar[pp][q] = ar[pp + 1][q];
+        if (v + 1 < NV) {
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
+        }
+        // transform pieces of chunk ck+1 (raw in R[(ck+1) & 1]) between the MFMA steps
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if ((WINO_ABLATE & 2) == 0 && more && v == (j * NV) / 4) job_piece(tb ^ 1, tb ^ 1, j);
+      }
+      if (P0 > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PD * NP) : "memory");  // raw(ck+2) landed
+      lds_sync();
+    }
+  };
+  if (grp == 0) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
+
+  // ---- epilogue ----
+  if (WINO_ABLATE & 16) {
+    float sum = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += acc[p][n][r];
+    if (sum == 1234.5f) a.y[threadIdx.x] = sum;
+    return;
+  }
+  const float sc = H3 ? ldexpf(1.f, ex + a.w_exp) : 1.f;
+  // partial outputs of this wave's points: yp[n][i][r]
+  float yp[2][4][16];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (grp == 0) {
+        const float m0 = acc[0][n][r] * sc, m1 = acc[1][n][r] * sc, m2 = acc[2][n][r] * sc, m3 = acc[3][n][r] * sc;
+        const float s12 = m1 + m2, d12 = m1 - m2;
+        yp[n][0][r] = (m0 + s12) + m3;
+        yp[n][1][r] = fmaf(2.f, m3, d12);
+        yp[n][2][r] = fmaf(4.f, m3, s12);
+        yp[n][3][r] = fmaf(8.f, m3, d12);
+      } else {
+        const float m4 = acc[0][n][r] * sc, m5 = acc[1][n][r] * sc, m6 = acc[2][n][r] * sc;
+        yp[n][0][r] = m4 + m5;
+        yp[n][1][r] = fmaf(-2.f, m4, 0.5f * m5);
+        yp[n][2][r] = fmaf(4.f, m4, 0.25f * m5);
+        yp[n][3][r] = fmaf(-8.f, m4, 0.125f * m5) + m6;
+      }
+    }
+  // swap halves: group 0 finishes column block 0, group 1 block 1 (two passes of 8 rows per lane)
+  const int nk = grp;
+  float y[4][16];
+  float* xch = reinterpret_cast<float*>(tsm);  // [wm][grp][8 r][4 i][64 lanes], 64 KiB
+  lds_sync();  // every wave is past its last LDS read of the main loop
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xch[((((wm * 2 + grp) * 8 + r) * 4 + i) * 64) + lane] = grp == 0 ? yp[1][i][8 * h + r] : yp[0][i][8 * h + r];
+    lds_sync();
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float other = xch[((((wm * 2 + (1 - grp)) * 8 + r) * 4 + i) * 64) + lane];
+        y[i][8 * h + r] = (grp == 0 ? yp[0][i][8 * h + r] : yp[1][i][8 * h + r]) + other;
+      }
+    lds_sync();
+  }
+
+  const int zm = a.zmode <= 1 ? 0 : a.zmode;
+  const int cobase = mt * 128 + wm * 32;
+  auto finish = [&](auto res_tag, auto zm_tag) {
+    constexpr bool RES = decltype(res_tag)::value;
+    constexpr int ZM = decltype(zm_tag)::value;
+    const int Cout = a.Cout;
+    const int Tout = a.Tout;
+    const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;
+    const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
+    const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
+    const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
+    const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
+    const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
+    const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
+                                 a.cvec ? (unsigned)Cout * 4u : 0u);
+    const float oslope = a.out_slope;
+    const float zdiv = a.zdiv;
+    float vmax = 0.f;
+    if constexpr (D == 1) {
+      const int t = t0 + 4 * (nk * 32 + l32);
+      const int nvalid = Tout - t < 4 ? (Tout - t > 0 ? Tout - t : 0) : 4;
+      const bool full = nvalid == 4 && (Tout & 3) == 0;
+#pragma unroll
+      for (int r0 = 0; r0 < 16; r0 += 8) {  // gather 8 vectors, then compute and store them
+        float bias[8];
+        unsigned voff[8];
+        WinoIn gin[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = r0 + k;
+          const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
+          bias[k] = bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
+          voff[k] = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+          gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = r0 + k;
+          const f32x4 yv = {y[0][r], y[1][r], y[2][r], y[3][r]};
+          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[k], oslope, zdiv, gin[k], nvalid, vmax);
+          wino_store(rout, v, voff[k], full, nvalid);
+        }
+      }
+    } else {
+      // pair region [16 rows][PITCH] per pass; the pair's two waves read 8 rows each
+      float* tile = reinterpret_cast<float*>(tsm) + wm * (16 * C::PITCH);
+      const int nn = nk * 32 + l32;
+      const int jj = nn / D, rho = nn - (nn / D) * D;
+      const int tl = 4 * lane;
+      const int t = t0 + tl;
+      const int lim = (C::TW < Tout - t0 ? C::TW : Tout - t0) - tl;
+      const int nvalid = lim < 4 ? (lim > 0 ? lim : 0) : 4;
+      const bool full = nvalid == 4 && (Tout & 3) == 0;
+#pragma unroll
+      for (int ps = 0; ps < 2; ++ps) {
+        if (jj < C::J) {
+#pragma unroll
+          for (int r = 8 * ps; r < 8 * ps + 8; ++r) {
+            const int rl = (r & 3) + 8 * ((r >> 2) - 2 * ps) + 4 * half;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tile[rl * C::PITCH + rho + D * (4 * jj + i)] = y[i][r];
+          }
+        }
+        lds_sync();
+        float bias[8];
+        unsigned voff[8];
+        WinoIn gin[8];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const int co = cobase + 16 * ps + grp * 8 + rr;
+          bias[rr] = bload(rbias, (unsigned)co * 4u, 0u) + bload(rcv, (unsigned)co * 4u, 0u);
+          voff[rr] = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+          gin[rr] = wino_gather<RES, ZM>(rres, rz, voff[rr], full, nvalid);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(tile + (grp * 8 + rr) * C::PITCH + tl);
+          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[rr], oslope, zdiv, gin[rr], nvalid, vmax);
+          wino_store(rout, v, voff[rr], full, nvalid);
+        }
+        lds_sync();
+      }
+    }
+    if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+  };
+  using BT = std::true_type;
+  using BF = std::false_type;
+  using Z0 = std::integral_constant<int, 0>;
+  using Z2 = std::integral_constant<int, 2>;
+  using Z3 = std::integral_constant<int, 3>;
+  if (a.res) {
+    if (zm == 0) finish(BT{}, Z0{});
+    else if (zm == 2) finish(BT{}, Z2{});
+    else finish(BT{}, Z3{});
+  } else {
+    if (zm == 0) finish(BF{}, Z0{});
+    else if (zm == 2) finish(BF{}, Z2{});
+    else finish(BF{}, Z3{});
+  }
+}
+
+namespace wino8_detail {
+template <class S, int K, int D>
+void launch_d(const Conv1dArgs& a, int B, hipStream_t s) {
+  using C = Wino8Cfg<S, K, D>;
+  const dim3 grid(ceil_div(a.Tout, C::TW), ceil_div(a.Cout, 128), B);
+  if constexpr (D == 1) {
+    if (a.in_slope == 1.f) {
+      hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, false>), grid, dim3(512), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, true>), grid, dim3(512), 0, s, a);
+}
+
+template <class S, int K>
+void launch_k(const Conv1dArgs& a, int B, hipStream_t s) {
+  switch (a.dil) {
+    case 1: launch_d<S, K, 1>(a, B, s); break;
+    case 3: launch_d<S, K, 3>(a, B, s); break;
+    case 5: launch_d<S, K, 5>(a, B, s); break;
+    default: throw Error(3, "conv1d(winograd8): dilation must be 1, 3 or 5");
+  }
+}
+
+template <class S>
+void launch_s(const Conv1dArgs& a, int B, int K, hipStream_t s) {
+  TTS_REQUIRE(a.mask == nullptr && a.ups == 0 && a.gate == 0 && a.rep_pad == 0 && a.Tin == a.Tout &&
+                  a.pad == a.dil * (K - 1) / 2 && a.Tin % 4 == 0,
+              1, "conv1d(winograd8): unsupported arguments");
+  switch (K) {
+    case 7: launch_k<S, 7>(a, B, s); break;
+    case 11: launch_k<S, 11>(a, B, s); break;
+    default: throw Error(3, "conv1d(winograd8): kernel size must be 7 or 11");
+  }
+}
+}  // namespace wino8_detail
+
+}  // namespace tts

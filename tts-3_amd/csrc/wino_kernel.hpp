@@ -31,7 +31,7 @@ namespace tts {
 
 #ifndef WINO_ABLATE
 #define WINO_ABLATE 0  // ablation builds (timing only, wrong results): 1 no x loads, 2 no transform jobs, 4 no A stream,
-                       // 8 no MFMA, 16 no epilogue
+                       // 8 no MFMA, 16 no epilogue, 32 no input DMA (wino8)
 #endif
 
 constexpr int kWinoPoints = 7;
@@ -119,28 +119,41 @@ struct WinoCfg {
 //   per pass, two passes; the 2-way bank conflicts of the scattered writes are free on ds_write_b32)
 //   and then stores one row per instruction.
 // Residual / z values are gathered before the stores of the same vector (res may alias y).
-template <bool RES, int ZM, bool H3>
-__device__ __forceinline__ f32x4 wino_finish(f32x4 y, float bias, float oslope, float zdiv, const rsrc_t& rres,
-                                              const rsrc_t& rz, unsigned voff, bool full, int nvalid, float& vm) {
-  f32x4 rv = {}, zv = {};
+// Loads of one output vector (residual / MRF sum), issued for every vector a thread stores
+// before its first store: a load cannot be hoisted above a store that may alias it, so a
+// load-compute-store sequence per vector pays one full memory latency per vector.
+struct WinoIn {
+  f32x4 rv, zv;
+};
+template <bool RES, int ZM>
+__device__ __forceinline__ WinoIn wino_gather(const rsrc_t& rres, const rsrc_t& rz, unsigned voff, bool full, int nvalid) {
+  WinoIn g;
+  g.rv = f32x4{};
+  g.zv = f32x4{};
   if (full) {
-    if (RES) rv = bload4(rres, voff, 0u);
-    if (ZM >= 2) zv = bload4(rz, voff, 0u);
+    if (RES) g.rv = bload4(rres, voff, 0u);
+    if (ZM >= 2) g.zv = bload4(rz, voff, 0u);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const unsigned o = j < nvalid ? voff + 4u * j : OOB_OFF;
-      if (RES) rv[j] = bload(rres, o, 0u);
-      if (ZM >= 2) zv[j] = bload(rz, o, 0u);
+      if (RES) g.rv[j] = bload(rres, o, 0u);
+      if (ZM >= 2) g.zv[j] = bload(rz, o, 0u);
     }
   }
+  return g;
+}
+
+template <bool RES, int ZM, bool H3>
+__device__ __forceinline__ f32x4 wino_apply(f32x4 y, float bias, float oslope, float zdiv, const WinoIn& g, int nvalid,
+                                             float& vm) {
   f32x4 v;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float x = lrelu2(y[j] + bias, oslope);
-    if (RES) x = x + rv[j];
-    if (ZM == 2) x = zv[j] + x;
-    if (ZM == 3) x = (zv[j] + x) / zdiv;
+    if (RES) x = x + g.rv[j];
+    if (ZM == 2) x = g.zv[j] + x;
+    if (ZM == 3) x = (g.zv[j] + x) / zdiv;
     if (H3 && j < nvalid) vm = fmaxf(vm, fabsf(x));
     v[j] = x;
   }
@@ -194,14 +207,24 @@ __device__ __forceinline__ void wino_epilogue(const Conv1dArgs& a, const f32x16 
       const int nvalid = Tout - t < 4 ? (Tout - t > 0 ? Tout - t : 0) : 4;
       const bool full = nvalid == 4 && (Tout & 3) == 0;  // 16-byte aligned rows
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
-        const unsigned voff = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-        float yy[4];
-        yval(n, r, yy);
-        const f32x4 y = {yy[0], yy[1], yy[2], yy[3]};
-        const f32x4 v = wino_finish<RES, ZM, H3>(y, bv[r], oslope, zdiv, rres, rz, voff, full, nvalid, vmax);
-        wino_store(rout, v, voff, full, nvalid);
+      for (int r0 = 0; r0 < 16; r0 += 8) {  // gather 8 vectors, then compute and store them
+        unsigned voff[8];
+        WinoIn gin[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = r0 + k;
+          const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
+          voff[k] = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+          gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float yy[4];
+          yval(n, r0 + k, yy);
+          const f32x4 y = {yy[0], yy[1], yy[2], yy[3]};
+          const f32x4 v = wino_apply<RES, ZM, H3>(y, bv[r0 + k], oslope, zdiv, gin[k], nvalid, vmax);
+          wino_store(rout, v, voff[k], full, nvalid);
+        }
       }
     }
   } else {
@@ -233,15 +256,23 @@ __device__ __forceinline__ void wino_epilogue(const Conv1dArgs& a, const f32x16 
         }
       }
       __syncthreads();
+      constexpr int NR = 16 / RPI;
+      float bias[NR];
+      unsigned voff[NR];
+      WinoIn gin[NR];
 #pragma unroll
-      for (int rr = 0; rr < 16; rr += RPI) {
-        const int rl = rr + lane / LPR;
-        const int co = cobase + 16 * ps + rl;
-        const float bias = bload(rbias, (unsigned)co * 4u, 0u) + bload(rcv, (unsigned)co * 4u, 0u);
-        const unsigned voff = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+      for (int k = 0; k < NR; ++k) {
+        const int co = cobase + 16 * ps + k * RPI + lane / LPR;
+        bias[k] = bload(rbias, (unsigned)co * 4u, 0u) + bload(rcv, (unsigned)co * 4u, 0u);
+        voff[k] = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+        gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
+      }
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {
+        const int rl = k * RPI + lane / LPR;
         const f32x4 y = *reinterpret_cast<const f32x4*>(tile + rl * PITCH + tl);
-        const f32x4 v = wino_finish<RES, ZM, H3>(y, bias, oslope, zdiv, rres, rz, voff, full, nvalid, vmax);
-        wino_store(rout, v, voff, full, nvalid);
+        const f32x4 v = wino_apply<RES, ZM, H3>(y, bias[k], oslope, zdiv, gin[k], nvalid, vmax);
+        wino_store(rout, v, voff[k], full, nvalid);
       }
     }
   }
@@ -434,7 +465,7 @@ __global__ __launch_bounds__(256, TN == 1 ? 2 : 1) void conv1d_wino_kernel(Conv1
 
 namespace wino_detail {
 #ifndef WINO_PD
-#define WINO_PD 3
+#define WINO_PD 2
 #endif
 #ifndef WINO_TN
 #define WINO_TN 1
