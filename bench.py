@@ -85,6 +85,18 @@ def dominant_kernel(rows):
     return name, f, fam
 
 
+def winograd_fields(fam_name: str, achieved: float, peak: float) -> dict:
+    """The Winograd F(4,4) convs ("mrf_wino_k<K>_c<C>", wino8_kernel.hpp) compute the same outputs
+    with 7*ceil(K/4)/4 instead of K products per (output, co, ci): `achieved` stays the algorithmic
+    (direct-conv) FLOP rate, and the MFMA work actually issued is reported next to it."""
+    if not fam_name.startswith("mrf_wino_k"):
+        return {"algorithm": "direct"}
+    K = int(fam_name.split("_k")[1].split("_")[0])
+    ratio = 7 * ((K + 3) // 4) / 4 / K
+    return {"algorithm": "winograd F(4,4)", "mfma_products_per_direct": ratio,
+            "mfma_executed_tflops": achieved * ratio, "mfma_executed_frac": achieved * ratio / peak}
+
+
 def cpu_baseline(budget_s: float):
     """Time the CPU oracle on a bounded sample of the same workload (rank 0, N=1)."""
     sys.path.insert(0, REPO)
@@ -526,6 +538,7 @@ def main():
                 "traffic": traffic,
                 "flops_per_launch": per_launch_flops,
                 "avg_launch_ms": avg_ms,
+                **winograd_fields(fam_name, achieved, MODE_PEAK[a.math_mode]),
             },
             "hbm_roofline_step": hbm,
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},

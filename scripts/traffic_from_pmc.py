@@ -33,7 +33,8 @@ def forward_names(mode):
         C //= 2
         names.append(f"ups_u{u}_c{C}")
         for k in V1["kernels"]:
-            names += [f"mrf_conv_k{k}_c{C}"] * 6
+            fam = "mrf_wino" if (mode == "f16x3" and C >= 128 and k in (7, 11)) else "mrf_conv"
+            names += [f"{fam}_k{k}_c{C}"] * 6
     names.append("conv_post")
     return names
 

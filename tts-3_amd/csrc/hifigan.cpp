@@ -116,8 +116,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     // the MRF convs at >= 128 channels (kernels 7 and 11): Winograd F(4,4) (wino8_kernel.hpp;
     // MI355X, B=32: k11 c128 2.20 -> 1.73 ms, k7 c128 1.56 -> 1.43, k11 c256 1.16 -> 0.80, k7 c256
     // 0.82 -> 0.60 per launch; TTS_MI355X_WINO=0 keeps the direct kernel)
-    if (std::string(fam) == "mrf_conv" && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil))
+    if (std::string(fam) == "mrf_conv" && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil)) {
       L.tile = kSplitWinoTile;
+      fam = "mrf_wino";
+    }
     const ConvTile t = conv_tile(lmode, L.tile);
     L.n_chunks = ceil_div(Cin, t.CK);
     L.w_numel = packed_conv_numel(lmode, Cout, Cin, K, t);

@@ -27,6 +27,19 @@ namespace tts {
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifndef WINO_STAMPS
+#define WINO_STAMPS 0  // diagnostic builds only: per-wave s_memtime stamps into Conv1dArgs::z (zmode 0)
+#endif
+// stamp slot i of this wave: z viewed as u64[workgroup][wave][32] (lane 0 stores)
+#define WSTAMP(i)                                                                                            \
+  do {                                                                                                       \
+    if (WINO_STAMPS && (threadIdx.x & 63) == 0) {                                                            \
+      const size_t wg = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);      \
+      reinterpret_cast<unsigned long long*>(a.z)[(wg * 8 + (threadIdx.x >> 6)) * 32 + (i)] =                   \
+          __builtin_amdgcn_s_memtime();                                                                      \
+    }                                                                                                        \
+  } while (0)
+
 template <class S, int K, int D>
 struct Wino8Cfg {
   static constexpr int NCH = wino_chunks(K);
@@ -49,7 +62,7 @@ struct Wino8Cfg {
   static constexpr int UNITS = XROWS * 4;            // (column, channel quad)
   static constexpr int UPW = (UNITS + 7) / 8;        // units per wave
   static constexpr int PITCH = 256;                  // epilogue transpose row (samples)
-  static_assert(UPW <= 64 && UNITS <= 256 + 64, "one transform round per wave");
+  static_assert(UPW <= 64 && UNITS <= 256 + 64 && NCH >= 2, "one transform round per wave; the DMA spreads over 3 steps");
   static_assert(TW <= PITCH, "");
   static_assert(2 * TSZ >= 4 * 16 * PITCH * 4 && 2 * TSZ >= 8 * 8 * 4 * 64 * 4, "epilogue LDS (transformed buffers)");
 };
@@ -63,7 +76,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_PD
 #define WINO8_PD 2
 #endif
-  constexpr int PD = WINO8_PD;
+#ifndef WINO8_PD1
+#define WINO8_PD1 6
+#endif
   __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
   __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
 
@@ -88,10 +103,11 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 
   // ---- input DMA (waves 4-7): raw[ch][RPITCH] fp32, window start ta = t0 - PAD - ROFF ----
   const int ta = t0 - C::PAD - C::ROFF;
-  auto dma = [&](int c, int rb) {
+  // DMA instructions i = wm + 4k of raw(c) -> R[rb], for k in [k0, k1) (wave-uniform)
+  auto dma = [&](int c, int rb, int k0 = 0, int k1 = 64) {
     const int c0 = c * 16;
     const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
-    for (int i = wm; i < C::NDMA; i += 4) {  // wave-uniform
+    for (int i = wm + 4 * k0; i < C::NDMA && i < wm + 4 * k1; i += 4) {
       const int f = i * 64 + lane;
       const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
       const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
@@ -104,9 +120,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_DENSE
 #define WINO8_DENSE 1
 #endif
-  // dense: waves 4-7 (fewer MFMAs) take units 0-255 with every lane, wave 3 the rest; else every
-  // wave takes UPW units (balanced, but only UPW of its 64 lanes active)
-  const int u = WINO8_DENSE ? (grp == 1 ? (wave - 4) * 64 + lane : (wave == 3 ? 256 + lane : C::UNITS))
+  // dense: waves 0-3 (which issue no HBM loads and so never wait on one) take units 0-255 with every
+  // lane, wave 4 the rest; else every wave takes UPW units (balanced, but only UPW of its 64 lanes
+  // active)
+  const int u = WINO8_DENSE ? (grp == 0 ? wave * 64 + lane : (wave == 4 ? 256 + lane : C::UNITS))
                             : wave * C::UPW + lane;
   const bool uok = (WINO8_DENSE || lane < C::UPW) && u < C::UNITS;
   const int urow = u >> 2, uq = u & 3;
@@ -148,6 +165,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   f32x16 acc[4][2];
 #pragma unroll
   for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = f32x16{};
+  WSTAMP(0);
 
   // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0
   if (grp == 1) {
@@ -155,10 +173,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     if (nc > 1) dma(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  WSTAMP(1);
   lds_sync();
 #pragma unroll
   for (int j = 0; j < 4; ++j) job_piece(0, 0, j);
   lds_sync();
+  WSTAMP(2);
 
   // the chunk loop of one point group (NPG points starting at P0); both groups run it with the
   // same barrier sequence
@@ -166,6 +186,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     constexpr int NPG = decltype(npg_tag)::value;
     constexpr int P0 = decltype(p0_tag)::value;
     constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
+    // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
+    // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
+    constexpr int PD = P0 > 0 ? WINO8_PD1 : WINO8_PD;
     auto aoff = [&](int ck, int v) {  // byte soffset of virtual step v of chunk ck (v may run past NV)
       const int ck2 = ck + v / NV, v2 = v % NV;
       // prefetches past the last chunk (never used) re-read step 0 instead of running off the array
@@ -189,13 +212,15 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       const int tb = ck & 1;
       const unsigned char* tl = tsm + tb * C::TSZ;
       const bool more = ck + 1 < nc;
-      if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc) dma(ck + 2, tb);  // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed)
       read_b(tl, 0, bcur);
+      if (ck < 8) WSTAMP(3 + 2 * ck);
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) ar[PD][q] = bload4(ra, avoff, aoff(ck, v + PD) + (unsigned)q * 1024u);
         if (v + 1 < NV) read_b(tl, v + 1, bnext);
+        // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed), two DMA instructions per step
+        if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc && v < 3) dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);
         __builtin_amdgcn_sched_barrier(0);
         const int p = v % NPG;
 #pragma unroll
@@ -220,7 +245,11 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
         for (int j = 0; j < 4; ++j)
           if ((WINO_ABLATE & 2) == 0 && more && v == (j * NV) / 4) job_piece(tb ^ 1, tb ^ 1, j);
       }
-      if (P0 > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PD * NP) : "memory");  // raw(ck+2) landed
+      // raw(ck+2) landed: at most the weight loads issued after the last DMA (steps 3.. of this chunk)
+      // may still be in flight
+      constexpr int NAFTER = (PD < NV - 3 ? PD : NV - 3) * NP;
+      if (P0 > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NAFTER) : "memory");
+      if (ck < 8) WSTAMP(4 + 2 * ck);
       lds_sync();
     }
   };
@@ -261,6 +290,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
         yp[n][3][r] = fmaf(-8.f, m4, 0.125f * m5) + m6;
       }
     }
+  WSTAMP(20);
   // swap halves: group 0 finishes column block 0, group 1 block 1 (two passes of 8 rows per lane)
   const int nk = grp;
   float y[4][16];
@@ -284,6 +314,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     lds_sync();
   }
 
+  WSTAMP(21);
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
   const int cobase = mt * 128 + wm * 32;
   auto finish = [&](auto res_tag, auto zm_tag) {
@@ -368,6 +399,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       }
     }
     if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+    WSTAMP(22);
   };
   using BT = std::true_type;
   using BF = std::false_type;
