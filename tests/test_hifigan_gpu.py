@@ -101,6 +101,11 @@ WINO_CASES = [
     (3, 144, 128, 252, 11, 1, 0.1, 0.1, False, 0),  # 9 channel chunks (odd)
     (1, 16, 128, 64, 11, 1, 0.1, 0.1, False, 0),    # one channel chunk
     (2, 32, 256, 300, 7, 3, 0.1, 1.0, True, 0),     # two channel chunks, 2 row blocks
+    # kernel 3 (one chunk of 4 taps, the 4th zero)
+    (2, 128, 128, 1024, 3, 5, 0.1, 0.1, False, 0),
+    (1, 256, 256, 516, 3, 1, 1.0, 1.0, True, 3),
+    (1, 128, 128, 777, 3, 3, 0.1, 0.1, True, 2),    # 4-wave form (T % 4 != 0)
+    (1, 128, 128, 4, 3, 1, 1.0, 1.0, True, 1),
 ]
 
 

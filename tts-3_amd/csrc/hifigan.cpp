@@ -113,10 +113,12 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
     L.mode = lmode;
     L.tile = conv_tile_for(lmode, Cout, K, Cin, dil, res);
-    // the MRF convs at >= 128 channels (kernels 7 and 11): Winograd F(4,4) (wino8_kernel.hpp;
+    // the MRF convs at >= 128 channels, kernels 7 and 11: Winograd F(4,4) (wino8_kernel.hpp;
     // MI355X, B=32: k11 c128 2.20 -> 1.73 ms, k7 c128 1.56 -> 1.43, k11 c256 1.16 -> 0.80, k7 c256
-    // 0.82 -> 0.60 per launch; TTS_MI355X_WINO=0 keeps the direct kernel)
-    if (std::string(fam) == "mrf_conv" && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil)) {
+    // 0.82 -> 0.60 per launch; TTS_MI355X_WINO=0 keeps the direct kernel).  Kernel 3 is supported
+    // but measured within 2-4% of the direct kernel (1.05 vs 1.07 ms at c128), not worth the
+    // Winograd rounding, so it stays direct.
+    if (std::string(fam) == "mrf_conv" && K >= 7 && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil)) {
       L.tile = kSplitWinoTile;
       fam = "mrf_wino";
     }

@@ -8,7 +8,7 @@
 namespace tts {
 
 bool wino_supported(int mode, int Cout, int Cin, int K, int dil) {
-  return mode == MATH_FP32_F16X3 && Cout % 128 == 0 && Cin % 16 == 0 && (K == 7 || K == 11) &&
+  return mode == MATH_FP32_F16X3 && Cout % 128 == 0 && Cin % 16 == 0 && (K == 3 || K == 7 || K == 11) &&
          (dil == 1 || dil == 3 || dil == 5);
 }
 

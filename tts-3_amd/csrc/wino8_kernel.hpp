@@ -62,7 +62,7 @@ struct Wino8Cfg {
   static constexpr int UNITS = XROWS * 4;            // (column, channel quad)
   static constexpr int UPW = (UNITS + 7) / 8;        // units per wave
   static constexpr int PITCH = 256;                  // epilogue transpose row (samples)
-  static_assert(UPW <= 64 && UNITS <= 256 + 64 && NCH >= 2, "one transform round per wave; the DMA spreads over 3 steps");
+  static_assert(UPW <= 64 && UNITS <= 256 + 64 && 3 * NCH >= 3, "one transform round per wave; the DMA spreads over 3 steps");
   static_assert(TW <= PITCH, "");
   static_assert(2 * TSZ >= 4 * 16 * PITCH * 4 && 2 * TSZ >= 8 * 8 * 4 * 64 * 4, "epilogue LDS (transformed buffers)");
 };
@@ -447,9 +447,10 @@ void launch_s(const Conv1dArgs& a, int B, int K, hipStream_t s) {
                   a.pad == a.dil * (K - 1) / 2 && a.Tin % 4 == 0,
               1, "conv1d(winograd8): unsupported arguments");
   switch (K) {
+    case 3: launch_k<S, 3>(a, B, s); break;
     case 7: launch_k<S, 7>(a, B, s); break;
     case 11: launch_k<S, 11>(a, B, s); break;
-    default: throw Error(3, "conv1d(winograd8): kernel size must be 7 or 11");
+    default: throw Error(3, "conv1d(winograd8): kernel size must be 3, 7 or 11");
   }
 }
 }  // namespace wino8_detail

@@ -502,9 +502,10 @@ void launch_wino_s(const Conv1dArgs& a, int B, int K, hipStream_t s) {
                   a.pad == a.dil * (K - 1) / 2,
               1, "conv1d(winograd): unsupported arguments");
   switch (K) {
+    case 3: launch_wino_k<S, 1>(a, B, s); break;
     case 7: launch_wino_k<S, 2>(a, B, s); break;
     case 11: launch_wino_k<S, 3>(a, B, s); break;
-    default: throw Error(3, "conv1d(winograd): kernel size must be 7 or 11");
+    default: throw Error(3, "conv1d(winograd): kernel size must be 3, 7 or 11");
   }
 }
 }  // namespace wino_detail
