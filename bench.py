@@ -69,7 +69,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
     p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
     p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r01.json"))
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r02.json"))
     return p.parse_args()
 
 
@@ -449,7 +449,7 @@ def main():
     achieved = per_launch_flops / (avg_ms / 1e3) / 1e12
     total_flops = sum(r["flops"] for r in rows)
     traffic = None
-    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r01.json)
+    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r02.json)
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
