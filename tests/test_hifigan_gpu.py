@@ -239,8 +239,9 @@ def test_generator_stage_parity(cuda_device):
 
 @pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3"])
 def test_generator_edge_lengths_vs_oracle(cuda_device, mode):
-    """Lengths around the tile edges of every kernel family, incl. the fused resblock kernels of the
-    split modes (224 / 96-column tiles at C=32 / C=64) and the streaming conv_post (1024 samples)."""
+    """Short and ragged lengths through every kernel family: the fused resblock kernels of the split
+    modes (pair tiles of 256 - (K-1) / 192 - (K-1) columns at C=32 / C=64, whole-block tiles of 232
+    columns at C=32 and 104 at C=64 / C=128), the Winograd convs and the streaming conv_post."""
     sd = synthetic.hifigan_state_dict(seed=31, weight_norm=False)
     g = HifiganGenerator(**V1, math_mode=mode)
     g.remove_weight_norm()
@@ -332,3 +333,23 @@ def test_winograd_generator_matches_direct(cuda_device, monkeypatch):
         outs.append(g.inference(mel.to(cuda_device)).cpu())
         assert_close_fp32(outs[-1], ref, f"wino={wino}")
     assert max_abs(outs[0].numpy(), outs[1].numpy()) < 2e-5
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16"])
+def test_whole_block_fusion_matches_unfused(cuda_device, monkeypatch, mode):
+    """The kernel-3 ResBlock1 as one launch (resblock3_kernel: C=32, 64 and 128) against the
+    per-iteration path (TTS_MI355X_RESBLOCK3=0) over several workgroups per utterance: both within
+    the mode's gates of the fp64 oracle, and within the mode's own error of each other."""
+    sd = synthetic.hifigan_state_dict(seed=41, weight_norm=False)
+    mel = synthetic.mel(2, 45, seed=3)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    outs = []
+    for policy in ("all", "0"):
+        monkeypatch.setenv("TTS_MI355X_RESBLOCK3", policy)
+        g = HifiganGenerator(**V1, math_mode=mode)
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs.append(g.inference(mel.to(cuda_device)).cpu())
+        assert_close_fp32(outs[-1], ref, f"{mode} resblock3={policy}", **tol(mode))
+    assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)

@@ -169,6 +169,9 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         // fused convs1 -> convs2 iterations (kernels_resblock.hip) where supported; they reuse the
         // conv packing, which needs 32-row blocks covering the channels and 16-channel groups
         rb.fused = pair_fusion;
+        // the whole-block kernel reads the packing as [32-row block][16-channel group][tap]: the
+        // conv tile must cover the channels without padding
+        bool tiles_ok = true;
         for (int m = 0; m < 3; ++m) {
           rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false, mode));
           src.push_back({w1[m], b1[m]});
@@ -177,21 +180,23 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
           for (int c = 0; c < 2; ++c) {
             const ConvTile t = conv_tile(mode, rb.convs[2 * m + c].tile);
             const int dil = rb.convs[2 * m].dil;
-            rb.fused = rb.fused && (fuse_all ? resblock_pair_supported(mode, ch, k, dil) : resblock_pair_preferred(mode, ch, k, dil)) && t.CK == 16 &&
-                       ceil_div(ch, t.BM) * t.BM == ch;
+            tiles_ok = tiles_ok && t.CK % 16 == 0 && ch % t.CK == 0 && ch % t.BM == 0;
+            rb.fused = rb.fused && t.CK == 16 && ceil_div(ch, t.BM) * t.BM == ch &&
+                       (fuse_all ? resblock_pair_supported(mode, ch, k, dil) : resblock_pair_preferred(mode, ch, k, dil));
           }
         }
+        rb.fused3 = pair_fusion && tiles_ok;
       } else {
         for (int m = 0; m < 2; ++m) {
           rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", true, mode));
           src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
         }
       }
-      if (cfg_.resblock_type == 1 && rb.fused) {
+      if (cfg_.resblock_type == 1 && rb.fused3) {
         // whole-block fusion (kernels_resblock.hip resblock3_kernel): TTS_MI355X_RESBLOCK3 =
-        // "0" off, "32" 32-channel blocks only, "all" every supported block (default; MI355X A/B
-        // scripts/ab_res3.sh: c32 k3 2.52 -> 1.87 ms, c64 k3 3.18 -> 2.93 ms per batch)
-        static const int policy = [] {
+        // "0" off, "<C>" blocks of at most C channels, "all" every supported block (default; MI355X
+        // A/B scripts/ab_res3.sh: c32 k3 2.52 -> 1.87 ms, c64 k3 3.18 -> 2.93 ms per batch)
+        const int policy = [] {  // read at create time (the tests switch it per generator)
           const char* e = std::getenv("TTS_MI355X_RESBLOCK3");
           if (!e) return 1 << 30;
           if (std::string(e) == "all") return 1 << 30;

@@ -3,34 +3,34 @@
 // in one kernel, so the intermediate xt never reaches HBM (per iteration the unfused path moves
 // five C-channel planes, this one three: x read twice, x' written once).
 //
-// A workgroup (4 waves) owns RP_BN = 224 output columns.  Phase 1 computes convs1 on RP_W = 256
-// columns (the 224 plus conv2's halo of up to 16 on each side, 2 blocks of 32 per wave), exactly
+// A workgroup (4 waves) owns RP_BN = RP_W - (K - 1) output columns.  Phase 1 computes convs1 on
+// RP_W = 256 (or 192) columns (the RP_BN plus conv2's halo of (K - 1) / 2 on each side), exactly
 // like conv1d_split_kernel (X staged per 16-channel chunk in LDS, weights streamed from L2).
 // Its epilogue applies the bias and the lrelu, zeroes columns outside [0, T) (conv2's zero
 // padding), splits the values into the scheme's pieces and stores them as conv2's B operand in
-// the LDS the X staging used.  Phase 2 runs convs2 over the same 256 columns from that buffer
-// (the last 32 are discarded) and finishes in conv_epilogue (bias, residual, MRF sum, statistics).
+// the LDS the X staging used.  Phase 2 runs convs2 over the same RP_W columns from that buffer
+// (the last K - 1 are discarded) and finishes in conv_epilogue (bias, residual, MRF sum, statistics).
 // f16x3: xt's scale is the workgroup's own power of two (block max-abs): every conv2 output sums
 // products of one workgroup's xt only, so the per-tile scale is exact and batch-invariant.
 // The residual x is re-read from global memory, so x and x' must not alias (ping-pong buffers).
+#include <algorithm>
 #include <cstdlib>
 
 #include "split_device.hpp"
 
 namespace tts {
 
-constexpr int RP_LEAD = 16;  // xt row 0 holds time t0 - RP_LEAD
-
 // Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
-// 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 32 output columns.
+// 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 2 * LEAD output columns.
 //   GEO 0: RP_W = 256, every wave all C rows x 64 columns (C = 32: 1 x 2 blocks, C = 64: 2 x 2)
 //   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
 //   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
-//   instead of 92 KB); the halo costs 1/6 of the columns instead of 1/8.
+//   instead of 92 KB); the halo costs (K - 1) / 192 of the columns instead of (K - 1) / 256.
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false>
 struct PairCfg {
   static constexpr int RP_W = GEO == 0 ? 256 : 192;
-  static constexpr int RP_BN = RP_W - 2 * RP_LEAD;
+  static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
+  static constexpr int RP_BN = RP_W - 2 * LEAD;
   static constexpr int WN = GEO == 0 ? 4 : 2;
   static constexpr int WM = 4 / WN;
   static constexpr int TM = C / 32 / WM;
@@ -46,7 +46,6 @@ struct PairCfg {
   static constexpr int XBUFS = ALLX ? NC : 2;
   static constexpr int LDSB = (XBUFS * XSZB > TSZB ? XBUFS * XSZB : TSZB);
   static constexpr int UPT = (XROWS * 4 + 255) / 256;
-  static_assert((K - 1) / 2 <= RP_LEAD, "conv2 halo");
   static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
@@ -77,7 +76,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
   const int d = a1.dil;
   const int T = a1.Tout;
   const int XW = RP_W + (K - 1) * d;
-  const int tx0 = t0 - RP_LEAD;  // time of convs1 column 0
+  const int tx0 = t0 - P::LEAD;  // time of convs1 column 0
   const unsigned avoff = (unsigned)lane * 16u;
 
   // ------------------------------------------------------------------ phase 1: convs1
@@ -286,7 +285,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
       for (int m = 0; m < TM; ++m)
 #pragma unroll
         for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
-    const int trow0 = xrow0 + RP_LEAD - (K - 1) / 2;
+    const int trow0 = xrow0;  // + LEAD - (K - 1) / 2
     auto read_t = [&](int g, int k, f32x4 (*dst)[NP]) {
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
@@ -401,9 +400,10 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
 // ---------------------------------------------------------------------------------------
 // Whole kernel-3 ResBlock1 (hifigan_generator.py:84-99, K = 3, dilations d0..d2) in one kernel:
 //   for m in 0..2:  xt = lrelu(convs1[m](lrelu(x)));  x = convs2[m](xt) + x;   z (+)= x
-// All three iterations run on the same RP_W-column grid (column c <-> time t0 - 16 + c): each conv
-// loses its halo at the grid edges, so the valid columns shrink by d_m + 1 per side per iteration
-// (12 for dilations 1, 3, 5) while the kept ones, [16, RP_W - 16), stay exact.  x lives in the
+// All three iterations run on the same RP_W-column grid (column c <-> time t0 - R3_LEAD + c): each
+// conv loses its halo at the grid edges, so the valid columns shrink by d_m + 1 per side per
+// iteration (11 for dilations 1, 3, 5: the first conv reads 5 staged extra columns, the rest only
+// the grid) while the kept ones, [R3_LEAD, RP_W - R3_LEAD), stay exact.  x lives in the
 // accumulator layout in registers (the residual of every iteration), lrelu(x) and xt alternate
 // in one LDS region as split B operands (X rows: column + 5, xt rows: column + 1).  Columns
 // outside the valid range or outside [0, T) are staged as zeros; in the f16x3 scheme the scale of
@@ -412,11 +412,14 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
 // x is read once and z written once instead of five C-planes per iteration.
 // ---------------------------------------------------------------------------------------
 constexpr int R3_XOFF = 5;  // X rows hold column + 5 (convs1 halo up to dilation 5)
+// kept columns [R3_LEAD, RP_W - R3_LEAD): only the first conv sees the R3_XOFF staged extra
+// columns, every later one loses d_m (+ 1) columns at the grid edge, 11 for dilations 1, 3, 5
+constexpr int R3_LEAD = 12;
 
 template <class S, int C, int GEO>
 struct Res3Cfg {
   static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
-  static constexpr int RP_BN = RP_W - 2 * RP_LEAD;
+  static constexpr int RP_BN = RP_W - 2 * R3_LEAD;
   static constexpr int WN = GEO == 0 ? 4 : 2;
   static constexpr int WM = 4 / WN;
   static constexpr int TM = C / 32 / WM;
@@ -428,7 +431,7 @@ struct Res3Cfg {
 };
 
 template <class S, int C, int GEO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 || GEO == 2 ? 2 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) ? 2 : 1)))
 void resblock3_kernel(ResBlock3Args a) {
   using P = Res3Cfg<S, C, GEO>;
   constexpr int K = 3;
@@ -450,7 +453,7 @@ void resblock3_kernel(ResBlock3Args a) {
   const int t0 = blockIdx.x * P::RP_BN;
   const int b = blockIdx.z;
   const int T = a.T;
-  const int tx0 = t0 - RP_LEAD;  // time of column 0
+  const int tx0 = t0 - R3_LEAD;  // time of column 0
   const int xcol0 = wn * TN * 32 + l32;
   const unsigned avoff = (unsigned)lane * 16u;
   const unsigned chb = (unsigned)T * 4u;
@@ -517,7 +520,6 @@ void resblock3_kernel(ResBlock3Args a) {
   f32x16 acc[TM][TN];
   f32x4 ar[PD + 1][TM][NP], bcur[TN][NP], bnext[TN][NP];
   rsrc_t ra[TM];
-  // one conv over the LDS region: B rows = column + roff + k * kstep
   auto conv = [&](int wi, int roff, int kstep) {
 #pragma unroll
     for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a.w[wi] + ((size_t)(wm * TM + m) * NC * K) * (NP * 256), 0xFFFFFFFFu);
@@ -548,7 +550,8 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
         for (int m = 0; m < TM; ++m)
 #pragma unroll
-          for (int q = 0; q < NP; ++q) ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((st + PD) * NP + q) * 1024u);
+          for (int q = 0; q < NP; ++q)
+            ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((st + PD) * NP + q) * 1024u);
         const bool more = (k + 1 < K) || (g + 1 < NC);
         if (more) read_b((k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
         __builtin_amdgcn_sched_barrier(0);
@@ -630,8 +633,8 @@ void resblock3_kernel(ResBlock3Args a) {
     const int d = a.dil[it];
     // ---- convs1[it] on lrelu(x) (X rows = column + 5): taps at column + (k - 1) * d
     conv(2 * it, R3_XOFF - d, d);
-    lo += d;
-    hi -= d;
+    lo = max(lo + d, 0);  // outputs exist on the grid [0, RP_W) only
+    hi = min(hi - d, RP_W);
     {
       const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it]) : 1.f;
       const rsrc_t rb = make_rsrc(a.bias[2 * it], (unsigned)C * 4u);
@@ -707,7 +710,7 @@ void resblock3_kernel(ResBlock3Args a) {
         for (int n = 0; n < TN; ++n) {
           const int col = xcol0 + n * 32;
           const int t = tx0 + col;
-          const bool keep = col >= RP_LEAD && col < RP_LEAD + P::RP_BN && t >= 0 && t < T;
+          const bool keep = col >= R3_LEAD && col < R3_LEAD + P::RP_BN && t >= 0 && t < T;
           unsigned vo[16];
           float zv[16];
 #pragma unroll
@@ -746,20 +749,24 @@ void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
     return (e && e[0] == '1') ? 1 : 2;
   }();
   if (C == 32) launch_res3_t<S, 32, 0>(a, B, s);
-  else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
+  else if (C == 128) {
+    // 192 columns (2 x 2 waves of 64 rows x 96 columns, one wave per SIMD); LDS 8 x 202 rows
+    if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 2>(a, B, s);
+  } else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
   else launch_res3_t<S, 64, 2>(a, B, s);
 }
 }  // namespace
 
 bool resblock3_supported(int mode, int C, int K, const int* dil) {
-  if (!is_split_mode(mode) || !(C == 32 || C == 64) || K != 3) return false;
-  int halo = 0;
+  // C = 128 stages 8 groups x 202 rows: 129 KB of LDS for f16x3 / 77 KB for bf16 (x6 does not fit)
+  if (!is_split_mode(mode) || !(C == 32 || C == 64 || (C == 128 && mode != MATH_FP32_X6)) || K != 3) return false;
+  // the kernel's valid-range walk: kept columns [R3_LEAD, RP_W - R3_LEAD) must stay inside it
+  int lo = -R3_XOFF;
   for (int m = 0; m < 3; ++m) {
     if (dil[m] < 1 || dil[m] > R3_XOFF) return false;
-    halo += dil[m] + 1;
+    lo = std::max(lo + dil[m], 0) + 1;
   }
-  // kept columns [16, RP_W - 16) must stay inside the valid range [-5 + halo, RP_W + 5 - halo)
-  return halo - R3_XOFF <= RP_LEAD;
+  return lo <= R3_LEAD;
 }
 
 void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s) {
