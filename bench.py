@@ -524,6 +524,8 @@ def main():
                 "parallelism": f"dp{world} (utterance sharding, no collectives)",
             },
             "rtf": rtf,
+            # samples of the unpadded mel (B * 256 * T), beside the padded numel above
+            "useful_samples_per_s": value * T / (T + 2 * pad),
             "model_tflops": total_flops / (ms_per_step / 1e3) / 1e12,
             "model_frac_fp32_peak": total_flops / (ms_per_step / 1e3) / 1e12 / FP32_PEAK_TFLOPS,
             "roofline": {

@@ -416,12 +416,18 @@ constexpr int R3_XOFF = 5;  // X rows hold column + 5 (convs1 halo up to dilatio
 // columns, every later one loses d_m (+ 1) columns at the grid edge, 11 for dilations 1, 3, 5
 constexpr int R3_LEAD = 12;
 
+// GEO 0: 256 columns, 4 waves side by side; GEO 1 / 2: 192 / 128 columns, 2 x 2 waves;
+// GEO 3: 128 columns, 8 waves (4 row blocks x 2 column halves at C = 128, two waves per SIMD).
+// Measured (f16x3, per batch): C = 128 GEO 3 5.0 ms vs GEO 2 5.5 ms; 8-wave forms at C = 64
+// (256 columns) and C = 32 (512 columns) were slower than GEO 2 / GEO 0 (+0.2 / +0.3 ms).
 template <class S, int C, int GEO>
 struct Res3Cfg {
   static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int RP_BN = RP_W - 2 * R3_LEAD;
+  static constexpr int NW = GEO == 3 ? 8 : 4;     // waves per workgroup
+  static constexpr int NT = 64 * NW;
   static constexpr int WN = GEO == 0 ? 4 : 2;
-  static constexpr int WM = 4 / WN;
+  static constexpr int WM = NW / WN;
   static constexpr int TM = C / 32 / WM;
   static constexpr int TN = RP_W / 32 / WN;
   static constexpr int NC = C / 16;
@@ -431,7 +437,8 @@ struct Res3Cfg {
 };
 
 template <class S, int C, int GEO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) ? 2 : 1)))
+__global__ __launch_bounds__((Res3Cfg<S, C, GEO>::NT))
+__attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) || GEO == 3 ? 2 : 1)))
 void resblock3_kernel(ResBlock3Args a) {
   using P = Res3Cfg<S, C, GEO>;
   constexpr int K = 3;
@@ -440,7 +447,8 @@ void resblock3_kernel(ResBlock3Args a) {
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC, PR = P::PR, RP_W = P::RP_W;
   constexpr int PD = 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
-  __shared__ float red[4];
+  constexpr int NT = P::NT;
+  __shared__ float red[P::NW];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -465,13 +473,13 @@ void resblock3_kernel(ResBlock3Args a) {
   int ex = H3 ? amax_exp(a.amax_in, b) : 0;
   {
     const float xs = H3 ? ldexpf(1.f, -ex) : 1.f;
-    constexpr int UG = (PR * 4 + 255) / 256;  // units (row, quad) per group per thread
+    constexpr int UG = (PR * 4 + NT - 1) / NT;  // units (row, quad) per group per thread
 #pragma unroll 1
     for (int g = 0; g < NC; ++g) {
       f32x4 xv[UG];
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
-        const int u = tid + i * 256;
+        const int u = tid + i * NT;
         const int q = u & 3;
         const int r = u >> 2;
         const int ts = tx0 - R3_XOFF + r;
@@ -482,7 +490,7 @@ void resblock3_kernel(ResBlock3Args a) {
       }
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
-        const int u = tid + i * 256;
+        const int u = tid + i * NT;
         const int q = u & 3;
         const int r = u >> 2;
         if (r < PR) {
@@ -584,7 +592,9 @@ void resblock3_kernel(ResBlock3Args a) {
     for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
     if (lane == 0) red[wave] = vmax;
     __syncthreads();  // also: every wave is done reading the LDS region
-    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float mx = red[0];
+#pragma unroll
+    for (int w = 1; w < P::NW; ++w) mx = fmaxf(mx, red[w]);
     __syncthreads();  // red[] is reused by the next call
     int e = 0;
     if (mx > 0.f && mx < INFINITY) {
@@ -616,7 +626,7 @@ void resblock3_kernel(ResBlock3Args a) {
       }
     // edge rows: [0, roff) and [roff + RP_W, PR) of every group
     constexpr int EB = 2 * R3_XOFF * S::ROWB;  // upper bound of edge bytes per group
-    for (int e = tid * 16; e < NC * EB; e += 256 * 16) {
+    for (int e = tid * 16; e < NC * EB; e += NT * 16) {
       const int g = e / EB;
       const int o = e - g * EB;  // byte in the edge area: first roff rows, then the tail
       const int lead_b = roff * S::ROWB;
@@ -738,7 +748,7 @@ namespace {
 template <class S, int C, int GEO>
 void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.T, Res3Cfg<S, C, GEO>::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO>), grid, dim3(Res3Cfg<S, C, GEO>::NT), 0, s, a);
 }
 template <class S>
 void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
@@ -748,17 +758,25 @@ void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
     const char* e = std::getenv("TTS_MI355X_RES3_GEO64");
     return (e && e[0] == '1') ? 1 : 2;
   }();
+  // C = 128: 128 columns as 8 waves of 32 rows x 64 columns (two per SIMD) unless
+  // TTS_MI355X_RES3_GEO128=2 (2 x 2 waves of 64 x 64, one per SIMD); LDS 8 x 138 rows either way
+  static const int geo128 = [] {
+    const char* e = std::getenv("TTS_MI355X_RES3_GEO128");
+    return (e && e[0] == '2') ? 2 : 3;
+  }();
   if (C == 32) launch_res3_t<S, 32, 0>(a, B, s);
   else if (C == 128) {
-    // 192 columns (2 x 2 waves of 64 rows x 96 columns, one wave per SIMD); LDS 8 x 202 rows
-    if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 2>(a, B, s);
+    if constexpr (S::ROWB <= 80) {
+      if (geo128 == 2) launch_res3_t<S, 128, 2>(a, B, s);
+      else launch_res3_t<S, 128, 3>(a, B, s);
+    }
   } else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
   else launch_res3_t<S, 64, 2>(a, B, s);
 }
 }  // namespace
 
 bool resblock3_supported(int mode, int C, int K, const int* dil) {
-  // C = 128 stages 8 groups x 202 rows: 129 KB of LDS for f16x3 / 77 KB for bf16 (x6 does not fit)
+  // C = 128 stages 8 groups x 138 rows: 88 KB of LDS for f16x3 / 53 KB for bf16 (x6 is not built)
   if (!is_split_mode(mode) || !(C == 32 || C == 64 || (C == 128 && mode != MATH_FP32_X6)) || K != 3) return false;
   // the kernel's valid-range walk: kept columns [R3_LEAD, RP_W - R3_LEAD) must stay inside it
   int lo = -R3_XOFF;
