@@ -79,6 +79,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_PD1
 #define WINO8_PD1 6
 #endif
+#ifndef WINO8_GAP7
+#define WINO8_GAP7 1
+#endif
+#ifndef WINO8_GAP11
+#define WINO8_GAP11 0
+#endif
   __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
   __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
 
@@ -129,15 +135,22 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const int urow = u >> 2, uq = u & 3;
   const int ujj = urow / D, urho = urow - (urow / D) * D;
   const int uri = urho + 4 * D * ujj + C::ROFF;  // raw index of the column's first input
-  float tkeep[7];
-  // piece j: channel 4q + j; pairs are written after channels 1 and 3
-  auto job_piece = [&](int rb, int tb, int j) {
+  float tkeep[7], jraw[7];
+  // piece j: channel 4q + j; pairs are written after channels 1 and 3.  A piece runs in two parts
+  // one MFMA step apart: job_load issues its 7 LDS reads, job_finish transforms (and splits and
+  // stores every second piece), so the reads' latency hides behind the step's MFMAs
+  auto job_load = [&](int rb, int j) {
     if (!uok) return;
     const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + j) * C::RPITCH + uri;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) jraw[k] = raw[D * k];
+  };
+  auto job_finish = [&](int tb, int j) {
+    if (!uok) return;
     float v[7], t[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      float x = raw[D * k];
+      float x = jraw[k];
       if (LRELU) x = lrelu2(x, slope);
       v[k] = H3 ? x * xscale : x;
     }
@@ -176,7 +189,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   WSTAMP(1);
   lds_sync();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) job_piece(0, 0, j);
+  for (int j = 0; j < 4; ++j) {
+    job_load(0, j);
+    job_finish(0, j);
+  }
   lds_sync();
   WSTAMP(2);
 
@@ -189,6 +205,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
     // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
     constexpr int PD = P0 > 0 ? WINO8_PD1 : WINO8_PD;
+    // steps between a transform piece's LDS reads and its math (no later than the next piece's
+    // reads); measured per kernel size
+    constexpr int GAP0 = K == 11 ? WINO8_GAP11 : WINO8_GAP7;
+    constexpr int GAP = GAP0 < NV / 4 ? GAP0 : NV / 4;
     auto aoff = [&](int ck, int v) {  // byte soffset of virtual step v of chunk ck (v may run past NV)
       const int ck2 = ck + v / NV, v2 = v % NV;
       // prefetches past the last chunk (never used) re-read step 0 instead of running off the array
@@ -240,10 +260,19 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
         }
-        // transform pieces of chunk ck+1 (raw in R[(ck+1) & 1]) between the MFMA steps
+        // transform pieces of chunk ck+1 (raw in R[(ck+1) & 1]) between the MFMA steps: piece j
+        // loads after step (j * NV) / 4 and finishes GAP steps later (0: at once)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if ((WINO_ABLATE & 2) == 0 && more && v == (j * NV) / 4) job_piece(tb ^ 1, tb ^ 1, j);
+        for (int j = 0; j < 4; ++j) {
+          const int vj = (j * NV) / 4;
+          if ((WINO_ABLATE & 2) == 0 && more) {
+            if (GAP > 0 && vj + GAP < NV && v == vj + GAP) job_finish(tb ^ 1, j);
+            if (v == vj) {
+              job_load(tb ^ 1, j);
+              if (GAP == 0 || vj + GAP >= NV) job_finish(tb ^ 1, j);
+            }
+          }
+        }
       }
       // raw(ck+2) landed: at most the weight loads issued after the last DMA (steps 3.. of this chunk)
       // may still be in flight
