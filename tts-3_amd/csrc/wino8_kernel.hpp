@@ -183,8 +183,13 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0
   if (grp == 1) {
     dma(0, 0);
-    if (nc > 1) dma(1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nc > 1) {
+      dma(1, 1);
+      // raw(0) only: a wave issues at least NDMA / 4 instructions of raw(1) after it (in order)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NDMA / 4) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   WSTAMP(1);
   lds_sync();
