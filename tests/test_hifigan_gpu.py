@@ -178,7 +178,7 @@ def test_op_conv_transpose1d(cuda_device, case, mode):
     assert_close_fp32(y.cpu(), ref, f"convT {case}", **tol(mode))
 
 
-@pytest.mark.parametrize("B,Cin,T", [(2, 32, 1000), (1, 32, 1), (3, 8, 513), (2, 64, 3001), (1, 20, 1024)])
+@pytest.mark.parametrize("B,Cin,T", [(2, 32, 1000), (1, 32, 1), (3, 8, 513), (2, 64, 3001), (1, 20, 1024), (2, 32, 2052), (1, 13, 4)])
 def test_op_conv_post(cuda_device, B, Cin, T):
     g = _rng(T)
     z = torch.randn(B, Cin, T, generator=g)

@@ -17,6 +17,9 @@
 // [CK][BN + (K-1)*dil] are staged in LDS once and reused by every tap and every wave.
 // Double-buffered: the next chunk is fetched to registers while the MFMAs run on the
 // current one; one barrier per chunk.
+#include <cstdint>
+#include <cstdlib>
+
 #include "conv_device.hpp"
 
 namespace tts {
@@ -467,6 +470,79 @@ __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
   for (int o = 0; o < 4; ++o) bstore(ry, tanhf(acc[o]), ti + o < T ? (unsigned)(ti + o) * 4u : OOB_OFF, 0u);
 }
 
+// T % 4 == 0 form (the generator's T = 256 * T'): no LDS window and no barrier in the channel
+// loop.  Each lane owns 4 consecutive samples and loads them per channel as one dwordx4; the 3
+// samples on either side come from the neighbour lanes (ds_bpermute), lanes 0 and 63 load the
+// vector beyond their wave's edge themselves (out-of-range vectors read as the zero padding).
+// 8 channels of loads are in flight ahead of the math.  Same FMA order as conv_post_kernel.
+constexpr int POST4_C = 8;
+__global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
+  __shared__ float ws[POST_MAXC * POST_K];
+  const int Cin = a.Cin;
+  const int T = a.T;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int b = blockIdx.y;
+  const int ti = blockIdx.x * POST_T + 4 * tid;
+  const rsrc_t rz = make_rsrc(a.z + (size_t)b * Cin * T, (unsigned)Cin * (unsigned)T * 4u);
+  const float slope = a.in_slope;
+  for (int e = tid; e < Cin * POST_K; e += 256) ws[e] = a.w[e];
+  const bool inb = ti < T;
+  const int te = lane == 0 ? ti - 4 : ti + 4;  // wave-edge vector (lanes 0 and 63 only)
+  const bool eok = (lane == 0 || lane == 63) && te >= 0 && te < T;
+  const int nb = (Cin + POST4_C - 1) / POST4_C;
+  f32x4 cm[POST4_C], ce[POST4_C], nm[POST4_C], ne[POST4_C];
+  auto load = [&](f32x4 (&m)[POST4_C], f32x4 (&e)[POST4_C], int cb) {
+#pragma unroll
+    for (int c = 0; c < POST4_C; ++c) {
+      const int ci = cb * POST4_C + c;
+      const unsigned row = (unsigned)ci * (unsigned)T;
+      m[c] = bload4(rz, (ci < Cin && inb) ? (row + (unsigned)ti) * 4u : OOB_OFF, 0u);
+      e[c] = bload4(rz, (ci < Cin && eok) ? (row + (unsigned)te) * 4u : OOB_OFF, 0u);
+    }
+  };
+  load(cm, ce, 0);
+  __syncthreads();  // ws
+  float acc[4] = {a.bias, a.bias, a.bias, a.bias};
+  for (int cb = 0; cb < nb; ++cb) {
+    if (cb + 1 < nb) load(nm, ne, cb + 1);
+#pragma unroll
+    for (int c = 0; c < POST4_C; ++c) {
+      const int ci = cb * POST4_C + c;
+      if (ci >= Cin) break;
+      float m[4], e[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        m[j] = lrelu(cm[c][j], slope);
+        e[j] = lrelu(ce[c][j], slope);
+      }
+      float row[12];  // times ti - 4 .. ti + 7 (row[0] and row[11] unused)
+      row[0] = row[11] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float l = __shfl(m[1 + j], lane - 1);
+        const float r = __shfl(m[j], lane + 1);
+        row[1 + j] = lane == 0 ? e[1 + j] : l;
+        row[8 + j] = lane == 63 ? e[j] : r;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) row[4 + j] = m[j];
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int k = 0; k < POST_K; ++k) acc[o] = fmaf(ws[ci * POST_K + k], row[1 + o + k], acc[o]);
+    }
+#pragma unroll
+    for (int c = 0; c < POST4_C; ++c) {
+      cm[c] = nm[c];
+      ce[c] = ne[c];
+    }
+  }
+  const rsrc_t ry = make_rsrc(a.y + (size_t)b * T, (unsigned)T * 4u);
+  const f32x4 yv = {tanhf(acc[0]), tanhf(acc[1]), tanhf(acc[2]), tanhf(acc[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, yv), ry, inb ? (int)((unsigned)ti * 4u) : (int)OOB_OFF, 0, 0);
+}
+
 __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const float* Wc, const float* bc,
                                                      float* cvec, int B, int Cc, int C0) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -628,11 +704,25 @@ void launch_convT(const ConvTArgs& a, int B, int U, int tile, hipStream_t s) {
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+// TTS_MI355X_POST4=0 keeps the LDS-window conv_post for every T (A/B runs)
+bool post4_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("TTS_MI355X_POST4");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+}  // namespace
+
 void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.Cin >= 1 && a.Cin <= POST_MAXC, 3, "conv_post: more than 64 input channels");
   TTS_REQUIRE((int64_t)a.Cin * a.T * 4 < (int64_t(1) << 31), 3, "conv_post: channel plane exceeds 2 GiB");
   dim3 grid(ceil_div(a.T, POST_T), B);
-  hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), 0, s, a);
+  // the vector form needs 16-byte aligned rows (T % 4 == 0) and plane bases
+  const bool vec = a.T % 4 == 0 && ((uintptr_t)a.z & 15) == 0 && ((uintptr_t)a.y & 15) == 0 && post4_enabled();
+  if (vec) hipLaunchKernelGGL(conv_post4_kernel, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), 0, s, a);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
