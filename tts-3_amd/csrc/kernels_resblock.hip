@@ -20,6 +20,10 @@
 
 namespace tts {
 
+#ifndef PAIR_PIPE
+#define PAIR_PIPE 0  // build option: 1 = software-pipelined epilogue gathers at 64 channels (measured neutral)
+#endif
+
 // Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
 // 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 2 * LEAD output columns.
 //   GEO 0: RP_W = 256, every wave all C rows x 64 columns (C = 32: 1 x 2 blocks, C = 64: 2 x 2)
@@ -61,9 +65,12 @@ void resblock_pair_kernel(ResPairArgs pa) {
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
   __shared__ float red[4];
+  __shared__ float bsm[2 * C];  // convs1 and convs2 biases (epilogue reads from LDS, not L2)
 
   const Conv1dArgs& a1 = pa.c1;
   const int tid = threadIdx.x;
+  const float bias1 = tid < C ? a1.bias[tid] : 0.f;
+  const float bias2 = tid < C ? pa.c2.bias[tid] : 0.f;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int half = lane >> 5;
@@ -180,6 +187,10 @@ void resblock_pair_kernel(ResPairArgs pa) {
     load_x(0);
     store_x(0, 0);
   }
+  if (tid < C) {
+    bsm[tid] = bias1;
+    bsm[C + tid] = bias2;
+  }
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -210,13 +221,12 @@ void resblock_pair_kernel(ResPairArgs pa) {
   // ------------------------------------------------------------------ convs1 epilogue -> xt (LDS)
   {
     const float sc1 = H3 ? ldexpf(1.f, ex + a1.w_exp) : 1.f;
-    const rsrc_t rb1 = make_rsrc(a1.bias, (unsigned)C * 4u);
     float tmax = 0.f;
 #pragma unroll
     for (int m = 0; m < TM; ++m) {
       float bv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bv[r] = bload(rb1, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+      for (int r = 0; r < 16; ++r) bv[r] = bsm[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
         const int t = tx0 + xrow0 + n * 32;
@@ -323,7 +333,8 @@ void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
         for (int n = 0; n < TN; ++n) acc[m][n] *= sc2;
     }
-    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN);
+    // C = 64: the software-pipelined epilogue (one memory latency per tile; registers allow it)
+    conv_epilogue<TM, TN, H3, C == 64 && PAIR_PIPE>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
   }
 }
 
@@ -390,6 +401,8 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
                   a.c2.Tout == a.c1.Tout && a.c1.rep_pad == 0 && a.c2.dil == 1,
               1, "resblock pair: bad arguments");
   TTS_REQUIRE(a.c2.res != a.c2.y || a.c2.zmode != 0, 1, "resblock pair: x and x' must not alias");
+  TTS_REQUIRE(a.c1.cvec == nullptr && a.c2.cvec == nullptr && a.c1.bias && a.c2.bias, 1,
+              "resblock pair: biases required, no cond vector (both are staged in LDS)");
   TTS_REQUIRE((int64_t)C * a.c1.Tout * 4 < (int64_t(1) << 31), 3, "resblock pair: plane exceeds 2 GiB");
   if (mode == MATH_FP32_F16X3) launch_pair_s<SchemeH3>(a, B, K, C, s);
   else if (mode == MATH_BF16) launch_pair_s<SchemeB1>(a, B, K, C, s);
@@ -449,6 +462,7 @@ void resblock3_kernel(ResBlock3Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
   constexpr int NT = P::NT;
   __shared__ float red[P::NW];
+  __shared__ float bsm[6 * C];  // the six conv biases (read by every epilogue: LDS, not L2, latency)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -468,15 +482,26 @@ void resblock3_kernel(ResBlock3Args a) {
   const float* xb = a.x + (size_t)b * C * T;
   const rsrc_t rx = make_rsrc(xb, (unsigned)C * chb);
 
-  // ---- prologue: lrelu(x0) pieces for columns [-5, RP_W + 5), one 16-channel group at a time,
-  // and x0 itself in the acc layout
+  // ---- prologue: lrelu(x0) pieces for columns [-5, RP_W + 5) of every 16-channel group, and x0
+  // itself in the acc layout.  Every load is issued before the first store (one HBM latency for
+  // the whole window instead of one per group: at C = 128 that is 8 groups, 64 VGPRs of window)
   int ex = H3 ? amax_exp(a.amax_in, b) : 0;
+  f32x16 xr[TM][TN];  // the running residual x (fp32), accumulator layout
   {
     const float xs = H3 ? ldexpf(1.f, -ex) : 1.f;
     constexpr int UG = (PR * 4 + NT - 1) / NT;  // units (row, quad) per group per thread
-#pragma unroll 1
-    for (int g = 0; g < NC; ++g) {
-      f32x4 xv[UG];
+    constexpr int BPT = (C + NT - 1) / NT;
+    float bl[6][BPT];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        const int e = tid + j * NT;
+        bl[i][j] = e < C ? a.bias[i][e] : 0.f;
+      }
+    f32x4 xv[NC][UG];
+#pragma unroll
+    for (int g = 0; g < NC; ++g)
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
         const int u = tid + i * NT;
@@ -486,8 +511,22 @@ void resblock3_kernel(ResBlock3Args a) {
         const bool ok = r < PR && ts >= 0 && ts < T;
         const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
+        for (int j = 0; j < 4; ++j) xv[g][i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
       }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int t = tx0 + xcol0 + n * 32;
+        const bool tok = t >= 0 && t < T;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+        }
+      }
+#pragma unroll
+    for (int g = 0; g < NC; ++g)
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
         const int u = tid + i * NT;
@@ -498,7 +537,7 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             unsigned short h[NP];
-            float v = lrelu2(xv[i][j], 0.1f);
+            float v = lrelu2(xv[g][i][j], 0.1f);
             if (H3) v *= xs;
             S::split(v, h);
 #pragma unroll
@@ -508,21 +547,14 @@ void resblock3_kernel(ResBlock3Args a) {
           for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(smem + (g * PR + r) * S::ROWB + 8 * q + 32 * p) = pv[p];
         }
       }
-    }
-  }
-  f32x16 xr[TM][TN];  // the running residual x (fp32), accumulator layout
 #pragma unroll
-  for (int m = 0; m < TM; ++m)
+    for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      const int t = tx0 + xcol0 + n * 32;
-      const bool tok = t >= 0 && t < T;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+      for (int j = 0; j < BPT; ++j) {
+        const int e = tid + j * NT;
+        if (e < C) bsm[i * C + e] = bl[i][j];
       }
-    }
+  }
   __syncthreads();
 
   f32x16 acc[TM][TN];
@@ -647,13 +679,13 @@ void resblock3_kernel(ResBlock3Args a) {
     hi = min(hi - d, RP_W);
     {
       const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it]) : 1.f;
-      const rsrc_t rb = make_rsrc(a.bias[2 * it], (unsigned)C * 4u);
+      const float* bs = bsm + (2 * it) * C;
       float vmax = 0.f;
 #pragma unroll
       for (int m = 0; m < TM; ++m) {
         float bv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
         for (int n = 0; n < TN; ++n) {
           const int col = xcol0 + n * 32;
@@ -679,14 +711,14 @@ void resblock3_kernel(ResBlock3Args a) {
     lo += 1;
     hi -= 1;
     const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it + 1]) : 1.f;
-    const rsrc_t rb = make_rsrc(a.bias[2 * it + 1], (unsigned)C * 4u);
+    const float* bs = bsm + (2 * it + 1) * C;
     if (it < 2) {
       float vmax = 0.f;
 #pragma unroll
       for (int m = 0; m < TM; ++m) {
         float bv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
         for (int n = 0; n < TN; ++n) {
           const int col = xcol0 + n * 32;
@@ -715,7 +747,7 @@ void resblock3_kernel(ResBlock3Args a) {
       for (int m = 0; m < TM; ++m) {
         float bv[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bload(rb, (unsigned)(mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
 #pragma unroll
         for (int n = 0; n < TN; ++n) {
           const int col = xcol0 + n * 32;
