@@ -71,11 +71,12 @@ __device__ __forceinline__ void publish_amax_block(unsigned* slots, int b, float
               __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
-// sbias: the bias already staged in LDS by the caller (no cvec then), else nullptr
+// sbias: bias + cvec of rows sbase.. already staged in LDS by the caller (rows >= Cout hold 0,
+// the same sums the two range-checked loads give), else nullptr
 template <int TM, int TN, bool RES, int ZM, bool AMAX>
 __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
                                                    int tbase, int cobase, int lane, int tend,
-                                                   const float* sbias) {
+                                                   const float* sbias, int sbase) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int Cout = a.Cout;
@@ -104,7 +105,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned co = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
-      bv[r] = sbias ? sbias[co] : bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
+      bv[r] = sbias ? sbias[(int)co - sbase] : bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
@@ -147,7 +148,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
 template <int TM, int TN, bool RES, int ZM, bool AMAX>
 __device__ __forceinline__ void conv_epilogue_pipe_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
                                                    int tbase, int cobase, int lane, int tend,
-                                                   const float* sbias) {
+                                                   const float* sbias, int sbase) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int Cout = a.Cout;
@@ -179,7 +180,7 @@ __device__ __forceinline__ void conv_epilogue_pipe_impl(const Conv1dArgs& a, con
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned co = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
-      bv[m][r] = sbias ? sbias[co] : bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
+      bv[m][r] = sbias ? sbias[(int)co - sbase] : bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
     }
   constexpr int NB = TM * TN;
   float rv[2][16], zv[2][16], mvb[2];
@@ -229,9 +230,11 @@ __device__ __forceinline__ void conv_epilogue_pipe_impl(const Conv1dArgs& a, con
 // Polyphase ConvTranspose1d epilogue (Conv1dArgs::ups = U): row rho = co*U + s, column frame m
 // -> y[b][co][U*m + s - U/2].  For U = 8 a lane's registers r = 4i..4i+3 hold the phases
 // 4*half .. 4*half+3 of one channel, i.e. 4 consecutive samples.
+// sb / scv: bias and cvec of rows sbase.. staged in LDS by the caller (or nullptr)
 template <int TM, int TN, bool AMAX>
 __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b, int tbase,
-                                               int cobase, int lane) {
+                                               int cobase, int lane, const float* sb = nullptr,
+                                               const float* scv = nullptr, int sbase = 0) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int U = a.ups;
@@ -251,8 +254,8 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned rho = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
-      bv[r] = bload(rbias, rho * 4u, 0u);
-      cv[r] = bload(rcv, (rho >> lgU) * 4u, 0u);
+      bv[r] = sb ? sb[(int)rho - sbase] : bload(rbias, rho * 4u, 0u);
+      cv[r] = sb ? scv[(int)rho - sbase] : bload(rcv, (rho >> lgU) * 4u, 0u);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
@@ -326,14 +329,14 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 template <int TM, int TN, bool AMAX = false, bool PIPE = false>
 __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
                                               int tbase, int cobase, int lane, int tend = 0x7fffffff,
-                                              const float* sbias = nullptr) {
+                                              const float* sbias = nullptr, int sbase = 0) {
   // copy the argument block: a store through `out` could alias it in the compiler's view
   const Conv1dArgs a = args;
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
 #define TTS_EPI(RES, ZM)                                                                  \
   do {                                                                                    \
-    if (PIPE) conv_epilogue_pipe_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias); \
-    else conv_epilogue_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias); \
+    if (PIPE) conv_epilogue_pipe_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase); \
+    else conv_epilogue_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase); \
   } while (0)
   if (a.res) {
     if (zm == 0) TTS_EPI(true, 0);

@@ -100,6 +100,13 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   // the gate epilogue reuses the staging buffers for its sigmoid exchange (32 KiB)
   constexpr int XCHB = GATE ? 4 * C::WN * TM * TN * 16 * 64 : 0;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB > XCHB ? 2 * C::XSZB : XCHB];
+  // bias (+ cvec) of this tile's BM rows, staged with the first input chunk: the epilogue then
+  // reads LDS instead of paying an L2 latency after the last MFMA (conv: the sum bias + cvec,
+  // as the epilogue's two range-checked loads give it; ConvTranspose: both, added in order)
+  // (only where the 0.5-1 KB does not cost a workgroup per CU: 160 KB of LDS per CU)
+  constexpr int LDS_MAIN = 2 * C::XSZB > XCHB ? 2 * C::XSZB : XCHB;
+  constexpr bool SB = !GATE && 163840 / LDS_MAIN == 163840 / (LDS_MAIN + BM * 4 * (K == 2 ? 2 : 1) + 64);
+  __shared__ float sbias[SB ? BM : 1], scvec[SB && K == 2 ? BM : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -231,8 +238,29 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     }
   };
 
+  float bpre = 0.f, cpre = 0.f;
+  if (SB && tid < BM) {
+    const int row = mt * BM + tid;
+    if (row < a.Cout) {
+      bpre = a.bias[row];
+      if (K == 2) {
+        const int co = row / a.ups;
+        cpre = a.cvec ? a.cvec[(size_t)b * (a.Cout / a.ups) + co] : 0.f;
+      } else {
+        cpre = a.cvec ? a.cvec[(size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)a.Cout) + row] : 0.f;
+      }
+    }
+  }
   load_x(0);
   store_x(0);
+  if (SB && tid < BM) {
+    if (K == 2) {
+      sbias[tid] = bpre;
+      scvec[K == 2 ? tid : 0] = cpre;
+    } else {
+      sbias[tid] = bpre + cpre;
+    }
+  }
   __syncthreads();
 
   for (int c = 0; c < nc; ++c) {
@@ -292,9 +320,9 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     static_assert(BM == 128 && C::WM == 2, "gate epilogue");
     gate_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt, wm, wn, lane, reinterpret_cast<float*>(smem));
   } else if constexpr (K == 2) {
-    convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+    convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr, SB ? scvec : nullptr, mt * BM);
   } else {
-    conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane);
+    conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, 0x7fffffff, SB ? sbias : nullptr, mt * BM);
   }
 }
 

@@ -87,6 +87,8 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #endif
   __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
   __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
+  __shared__ float wbias[128];  // bias + cvec of the 128 rows, staged in the prologue (the epilogue
+                                // reads LDS instead of paying an L2 latency per pass)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -180,6 +182,15 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = f32x16{};
   WSTAMP(0);
 
+  float bpre = 0.f;
+  if (tid < 128) {
+    const int co = mt * 128 + tid;
+    if (co < a.Cout) {
+      bpre = a.bias[co];
+      const float cv = a.cvec ? a.cvec[(size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)a.Cout) + co] : 0.f;
+      bpre = bpre + cv;  // the sum the two range-checked epilogue loads gave
+    }
+  }
   // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0
   if (grp == 1) {
     dma(0, 0);
@@ -192,6 +203,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     }
   }
   WSTAMP(1);
+  if (tid < 128) wbias[tid] = bpre;
   lds_sync();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -361,9 +373,6 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
     const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
     const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
-    const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
-    const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
-                                 a.cvec ? (unsigned)Cout * 4u : 0u);
     const float oslope = a.out_slope;
     const float zdiv = a.zdiv;
     float vmax = 0.f;
@@ -380,7 +389,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
         for (int k = 0; k < 8; ++k) {
           const int r = r0 + k;
           const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
-          bias[k] = bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
+          bias[k] = wbias[co - (unsigned)(mt * 128)];
           voff[k] = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
           gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
         }
@@ -419,7 +428,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
           const int co = cobase + 16 * ps + grp * 8 + rr;
-          bias[rr] = bload(rbias, (unsigned)co * 4u, 0u) + bload(rcv, (unsigned)co * 4u, 0u);
+          bias[rr] = wbias[co - mt * 128];
           voff[rr] = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
           gin[rr] = wino_gather<RES, ZM>(rres, rz, voff[rr], full, nvalid);
         }
