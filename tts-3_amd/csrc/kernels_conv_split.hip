@@ -99,12 +99,27 @@ int conv1d_split_num_tiles(int mode) {
   return kNumSplitTiles;
 }
 
+namespace {
+int env_tile(const char* name) {  // a plain split tile index from the environment, else -1
+  const char* e = std::getenv(name);
+  const int t = e ? std::atoi(e) : -1;
+  return (t >= 0 && t < kNumSplitTiles && t != kSplitGateTile && t != kSplitWinoTile) ? t : -1;
+}
+}  // namespace
+
 // Tile choice per conv shape from the round-1 MI355X sweeps (profiles/r01_tune_conv_*.log).
 // Any tile is correct for any Cin: channels past Cin read 0.
 int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
   (void)res;
   if ((K - 1) * dil > (K - 1) * 5) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
   if (mode == MATH_FP32_F16X3) {
+    // TTS_MI355X_TILE_UPS64 / TTS_MI355X_TILE_UPSBIG=<idx> override the ConvTranspose tiles
+    // (K == 2, U*Cout rows <= 64 / > 64; A/B runs)
+    if (K == 2) {
+      static const int ups64 = env_tile("TTS_MI355X_TILE_UPS64"), upsbig = env_tile("TTS_MI355X_TILE_UPSBIG");
+      const int t = Cout <= 64 ? ups64 : upsbig;
+      if (t >= 0) return t;
+    }
     // TTS_MI355X_TILE_BIG=<idx> overrides the tile of the Cout > 64 layers (A/B runs)
     static const int big = [] {
       const char* e = std::getenv("TTS_MI355X_TILE_BIG");
