@@ -3,21 +3,32 @@
 
 One "step" = ``HifiganGenerator.inference`` on a resident [32, 80, 1024] fp32 mel batch
 (replicate pad 5 -> 1034 frames -> 32 x 264,704 output samples), through the C-ABI library.
-One process per GPU; with N GPUs every rank vocodes its own 32-utterance shard (weak
-scaling, config 4's 256 utterances at N=8, no exchange step on the data path).
+One process per GPU.  ``--gpus N`` with N > 1 and no torchrun environment starts N rank
+processes itself (``torch.distributed.run``, before anything touches the GPU); under torchrun
+WORLD_SIZE must equal N.  At N > 1 one step is config 4's serving shape: rank 0 holds the
+whole 32*N-utterance mel batch in HBM, scatters one 32-utterance shard to every rank (RCCL over
+xGMI), every rank vocodes its shard, and rank 0 gathers the waveforms (weak scaling: 256
+utterances at N=8).  The compute-only step (each rank on its resident shard) and the scatter /
+gather times are reported beside it.
 
 Prints ONE JSON line (rank 0) with the driver contract fields plus:
   roofline     : the dominant kernel family's algorithmic FLOP/s (hipEvent-timed inside one
                  profiled forward, on the stream the kernels run on) vs the 157.3 TF fp32 peak
   cpu_baseline : the CPU oracle (oracle/hifigan_ref.py, torch.nn.functional fp32, the same
-                 ATen kernels as the reference) on a bounded sample, rank 0 at N=1 only
+                 ATen kernels as the reference) on the first utterances of the bench's own mel
+                 batch (median of 3 runs after one warm-up), rank 0 at N=1 only
+  build        : provenance of the loaded library (source hash stamped at build time, .so sha256)
 """
 from __future__ import annotations
 
 import argparse
 import contextlib
+import faulthandler
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -60,8 +71,6 @@ def parse():
     p.add_argument("--frames", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    p.add_argument("--comm", action="store_true",
-                   help="also time an RCCL scatter of mels / gather of wavs from rank 0 (reported separately)")
     p.add_argument("--math-mode", default="f16x3", choices=sorted(MODE_PEAK),
                    help="conv contraction arithmetic (see include/tts_mi355x.h TTS_MATH_*)")
     p.add_argument("--no-alt", action="store_true", help="skip the secondary run in the other math mode")
@@ -69,8 +78,43 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
     p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
     p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r02.json"))
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r03.json"))
+    p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r03.json"),
+                   help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
+    p.add_argument("--cpu-utts", type=int, default=2, help="utterances of the bench batch the CPU baseline vocodes")
+    p.add_argument("--comm-timeout", type=float, default=300.0, help="collective timeout (s), fail-fast")
+    p.add_argument("--rank-timeout", type=float, default=1500.0,
+                   help="a rank that runs longer than this dumps its stack and exits (hung peer)")
+    p.add_argument("--stub", action="store_true",
+                   help="TEST ONLY: CPU stand-in vocoder over gloo (exercises the launcher and sharding "
+                        "path without a GPU; its numbers are not a measurement)")
     return p.parse_args()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """--gpus N without a torchrun environment: run N ranks under torch.distributed.run as a
+    child process group (nothing in this process has touched the GPU) and return its status.
+    A launch that outlives --rank-timeout + 120 s is killed as a whole."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return p.wait(timeout=a.rank_timeout + 120)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, 9)
+        p.wait()
+        print(f"bench.py: {a.gpus}-rank launch timed out", file=sys.stderr)
+        return 124
 
 
 def dominant_kernel(rows):
@@ -97,8 +141,10 @@ def winograd_fields(fam_name: str, achieved: float, peak: float) -> dict:
             "mfma_executed_tflops": achieved * ratio, "mfma_executed_frac": achieved * ratio / peak}
 
 
-def cpu_baseline(budget_s: float):
-    """Time the CPU oracle on a bounded sample of the same workload (rank 0, N=1)."""
+def cpu_baseline(mel, n_utts: int, pad: int = 5):
+    """Time the CPU oracle on the first ``n_utts`` utterances of the bench's own mel batch (rank 0,
+    N=1): one warm-up on one utterance, then the median of 3 runs (same inputs as the
+    GPU run, median of >= 3)."""
     sys.path.insert(0, REPO)
     from oracle import hifigan_ref  # test infrastructure: the baseline being timed, not the product
     from tts_amd import synthetic
@@ -110,25 +156,26 @@ def cpu_baseline(budget_s: float):
     cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
     sd = synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False)
     sd = {k: v.float() for k, v in sd.items()}
-    B, T = 1, 256
-    mel = synthetic.mel(B, T, seed=0)
+    x = mel[:n_utts].cpu().contiguous()
+    B, _, T = x.shape
+    runs = []
     with torch.no_grad():
-        hifigan_ref.hifigan_forward(sd, mel[:, :, :8], pad=5, dtype=torch.float32, **cfg)  # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float32, **cfg)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= budget_s or n >= 1000:
-                break
-    samples = n * B * 256 * (T + 10)
+        hifigan_ref.hifigan_forward(sd, x[:1], pad=pad, dtype=torch.float32, **cfg)  # warm-up
+        for _ in range(3):
+            t0 = time.perf_counter()
+            hifigan_ref.hifigan_forward(sd, x, pad=pad, dtype=torch.float32, **cfg)
+            runs.append(time.perf_counter() - t0)
+    el = statistics.median(runs)
+    samples = B * 256 * (T + 2 * pad)
     return {
         "value": samples / el,
         "unit": "samples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} x HifiganGenerator.inference on [1,80,{T}] (oracle/hifigan_ref.py, torch-CPU fp32, "
-                  f"{threads} threads, {el:.1f} s)",
+        "sample": f"HifiganGenerator.inference on mel[0:{B}] of the bench batch ([{B},80,{T}] of "
+                  f"[{mel.shape[0]},80,{T}]), oracle/hifigan_ref.py torch-CPU fp32, {threads} threads, "
+                  f"median of 3 runs after 1 warm-up",
+        "runs_s": runs,
         "rtf": el / (samples / SAMPLE_RATE),
     }
 
@@ -147,25 +194,51 @@ def build_generator(math_mode, dev):
     return g.to(dev)
 
 
-def time_steps(g, mel, steps, warmup, dev, world):
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed(fn, steps, warmup, dev, world):
+    """W untimed calls, then K calls bracketed by barrier + device sync on both sides; the
+    max over ranks of the wall time, per call, in ms."""
     for _ in range(warmup):
-        g.inference(mel)
-    torch.cuda.synchronize(dev)
+        fn()
+    sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        g.inference(mel)
-    torch.cuda.synchronize(dev)
+        fn()
+    sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync(dev)
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()) / steps * 1e3
+
+
+def time_steps(g, mel, steps, warmup, dev, world):
+    return timed(lambda: g.inference(mel), steps, warmup, dev, world)
+
+
+class StubVocoder:
+    """TEST ONLY (--stub): a CPU stand-in with the generator's call surface and output shape
+    (hop 256, replicate pad 5), so the launcher / scatter / gather path runs without a GPU."""
+    hop_length = 256
+    inference_padding = 5
+
+    def inference(self, mel):
+        B, _, T = mel.shape
+        x = torch.nn.functional.pad(mel, (5, 5), mode="replicate").mean(1, keepdim=True)
+        return torch.tanh(x).repeat_interleave(self.hop_length, dim=2)
+
+    def reserve(self, B, T):
+        pass
 
 
 def accuracy_check(gens, dev):
@@ -242,19 +315,20 @@ def glow_bench(dev, math_mode, steps=10, warmup=3, B=16, T=768, cpu=True):
         sys.path.insert(0, REPO)
         from oracle import glow_ref  # test infrastructure: the baseline being timed, not the product
 
-        xs = x[:2].cpu()
-        ms_ = m[:2].cpu()
-        glow_ref.glow_decoder_reverse(sd, xs[:, :, :64], ms_[:, :, :64], dtype=torch.float32, **cfg)
-        n, c0 = 0, time.perf_counter()
+        xs = x.cpu()
+        ms_ = m.cpu()
+        runs = []
         with torch.no_grad():
-            while True:
+            glow_ref.glow_decoder_reverse(sd, xs, ms_, dtype=torch.float32, **cfg)  # warm-up
+            for _ in range(3):
+                c0 = time.perf_counter()
                 glow_ref.glow_decoder_reverse(sd, xs, ms_, dtype=torch.float32, **cfg)
-                n += 1
-                if time.perf_counter() - c0 > 5.0:
-                    break
-        el = time.perf_counter() - c0
-        out["cpu_baseline"] = {"mel_frames_per_s": n * 2 * T / el, "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"{n} x Decoder.forward(reverse=True) on [2,80,{T}] (oracle/glow_ref.py fp32)"}
+                runs.append(time.perf_counter() - c0)
+        el = statistics.median(runs)
+        out["cpu_baseline"] = {"mel_frames_per_s": B * T / el, "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"Decoder.forward(reverse=True) on the same [{B},80,{T}] input "
+                                         f"(oracle/glow_ref.py fp32), median of 3 runs after 1 warm-up",
+                               "runs_s": runs}
     return out
 
 
@@ -403,41 +477,146 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
     return out
 
 
+def rank_devices(world, rank, local, dev):
+    """Every rank's (rank, local rank, device, PCI bus) as torch.distributed saw it."""
+    me = {"rank": rank, "local_rank": local, "device": str(dev)}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        me.update(name=p.name, pci_bus_id=getattr(p, "pci_bus_id", None), gcn_arch=getattr(p, "gcnArchName", None))
+    if world == 1:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
+
+
+def sharded_step_bench(g, B, T, dev, world, rank, steps, warmup):
+    """Config 4: rank 0 holds [B*world, 80, T] in HBM; one step = scatter the mel shards ->
+    every rank vocodes B utterances -> gather the waveforms on rank 0.  Also times the scatter
+    and the gather alone."""
+    from tts_amd import synthetic
+    from tts_amd.sharding import gather_batch, scatter_batch
+
+    n = B * world
+    S = g.hop_length * (T + 2 * g.inference_padding)
+    full = synthetic.mel(n, T, seed=0).to(dev) if rank == 0 else None
+    shard = torch.empty(B, 80, T, device=dev)
+    wav = g.inference(shard.zero_())
+    wav_full = torch.empty(n, 1, S, device=dev) if rank == 0 else None
+
+    def step():
+        x = scatter_batch(full, n, (80, T), dev, out=shard)
+        gather_batch(g.inference(x), n, out=wav_full)
+
+    ms = timed(step, steps, warmup, dev, world)
+    scatter_ms = timed(lambda: scatter_batch(full, n, (80, T), dev, out=shard), max(3, steps), 1, dev, world)
+    gather_ms = timed(lambda: gather_batch(wav, n, out=wav_full), max(3, steps), 1, dev, world)
+    # parity of the sharded path: rank 0's gathered rows equal each shard vocoded alone (the
+    # generator is batch-invariant bit for bit, DESIGN §2)
+    step()
+    check = None
+    if rank == 0:
+        check = bool(torch.equal(wav_full[-B:], g.inference(full[-B:])))
+    return {"ms": ms, "scatter_ms": scatter_ms, "gather_ms": gather_ms, "utterances": n,
+            "mel_bytes": 4 * n * 80 * T, "wav_bytes": 4 * n * S, "last_shard_bitwise_equal": check}
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))  # before anything touches the GPU
+    world = int(env_world or 1)
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    faulthandler.dump_traceback_later(a.rank_timeout, exit=True)  # a hung peer ends this rank
+    if a.stub:
+        dev = torch.device("cpu")
+        if world > 1:
+            from tts_amd.sharding import init_distributed
+            init_distributed("gloo", local, a.comm_timeout)
+        g = StubVocoder()
+    else:
+        dev = torch.device("cuda", local)
+        if world > 1:
+            from tts_amd.sharding import init_distributed
+            init_distributed("nccl", local, a.comm_timeout)
+        g = build_generator(a.math_mode, dev)
+    devices = rank_devices(world, rank, local, dev)
+    real_world = dist.get_world_size() if world > 1 else 1
 
     from tts_amd import synthetic
 
-    g = build_generator(a.math_mode, dev)
     B, T, pad = a.batch, a.frames, g.inference_padding
-    mel = synthetic.mel(B, T, seed=rank).to(dev)
-    g.reserve(B, T)
-    torch.cuda.synchronize(dev)
-    ms_per_step = time_steps(g, mel, a.steps, a.warmup, dev, world)
     samples_per_step = B * g.hop_length * (T + 2 * pad)  # per GPU
+    mel = synthetic.mel(B, T, seed=rank).to(dev)  # this rank's resident shard
+    g.reserve(B, T)
+    sync(dev)
+    compute_ms = time_steps(g, mel, a.steps, a.warmup, dev, world)
+    shard = None
+    if world > 1:
+        shard = sharded_step_bench(g, B, T, dev, world, rank, a.steps, a.warmup)
+        ms_per_step = shard["ms"]
+    else:
+        ms_per_step = compute_ms
     value = world * samples_per_step / (ms_per_step / 1e3)
     rtf = (ms_per_step / 1e3) / (world * samples_per_step / SAMPLE_RATE)
 
-    comm = None
-    if a.comm and world > 1:
-        from tts_amd.sharding import gather_batch, scatter_batch
+    rec = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "samples/s",
+        "n_gpus": real_world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": DTYPE[a.math_mode],
+        "math_mode": a.math_mode,
+        "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
+        "config": {
+            "workload": f"HiFiGAN-v1 22.05kHz inference, [{B},80,{T}] mel per GPU (replicate pad 5), fp32"
+                        + (f"; config 4: rank 0 scatters [{B * world},80,{T}] and gathers the waveforms (RCCL)"
+                           if world > 1 else ""),
+            "model": "HiFiGAN-v1 (hifigan_config.py generator_model_params)",
+            "global_batch": B * world,
+            "seq_len": T,
+            "parallelism": f"dp{world} (utterance sharding; " + ("RCCL scatter/gather from rank 0)" if world > 1
+                                                                 else "no collectives)"),
+        },
+        "rtf": rtf,
+        # SURVEY 8(d): samples of the unpadded mel (B * 256 * T), beside the padded numel above
+        "useful_samples_per_s": value * T / (T + 2 * pad),
+        "world_size": real_world,
+        "devices": devices,
+    }
+    if shard is not None:
+        rec["sharded"] = {
+            "compute_only_ms_per_step": compute_ms,
+            "compute_only_value": world * samples_per_step / (compute_ms / 1e3),
+            "scatter_ms": shard["scatter_ms"], "gather_ms": shard["gather_ms"],
+            "comm_share_of_step": (shard["scatter_ms"] + shard["gather_ms"]) / ms_per_step,
+            "utterances": shard["utterances"], "mel_bytes": shard["mel_bytes"], "wav_bytes": shard["wav_bytes"],
+            "last_shard_bitwise_equal": shard["last_shard_bitwise_equal"],
+        }
+    if a.stub:
+        rec["data"] = "STUB (test only): CPU stand-in vocoder, not a measurement"
+        rec["dtype"] = "fp32"
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
-        n = B * world
-        full = synthetic.mel(n, T, seed=99).to(dev) if rank == 0 else None
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        c0 = time.perf_counter()
-        shard = scatter_batch(full, n, (80, T), dev)
-        gather_batch(g.inference(shard), n)
-        torch.cuda.synchronize(dev)
-        comm = {"scatter_infer_gather_ms": (time.perf_counter() - c0) * 1e3, "utterances": n}
+    from tts_amd import _native
+
+    rec["build"] = _native.build_info()
 
     # dominant-kernel roofline from one profiled forward (hipEvents per launch)
     _, rows = g.profile(mel)
@@ -449,7 +628,7 @@ def main():
     achieved = per_launch_flops / (avg_ms / 1e3) / 1e12
     total_flops = sum(r["flops"] for r in rows)
     traffic = None
-    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r02.json)
+    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r03.json)
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
@@ -457,8 +636,19 @@ def main():
             fwd_bytes = tj.get("per_launch_bytes", {}).get(f"{a.math_mode}:__forward__")
         except Exception:
             traffic = None
+    busy = {}
+    if os.path.exists(a.mfma_json):
+        try:
+            mj = json.load(open(a.mfma_json))
+            fb = mj.get("families", {}).get(f"{a.math_mode}:{fam_name}")
+            if fb:
+                busy = {"mfma_busy_frac": fb["mfma_busy_frac"], "clock_ghz": fb["clock_ghz"],
+                        "mfma_busy_frac_at_clock": fb.get("mfma_busy_frac_at_clock"),
+                        "mfma_busy_source": os.path.relpath(a.mfma_json, REPO)}
+        except Exception:
+            busy = {}
     algo_bytes = sum(r["bytes"] for r in rows)  # compulsory activation/weight bytes per launch, summed
-    step_s = ms_per_step / 1e3
+    step_s = compute_ms / 1e3
     hbm = {
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -471,7 +661,7 @@ def main():
 
     alt = None
     gens = {a.math_mode: g}
-    if not a.no_alt:
+    if not a.no_alt and world == 1:
         other = "fp32" if a.math_mode != "fp32" else "fp32x6"
         g2 = build_generator(other, dev)
         g2.reserve(B, T)
@@ -483,51 +673,19 @@ def main():
     acc = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         acc = accuracy_check(gens, dev)
-        cpu = cpu_baseline(a.cpu_seconds)
+        cpu = cpu_baseline(mel, a.cpu_utts, pad)
 
-    glow = None
-    if rank == 0 and not a.no_glow:
-        glow = glow_bench(dev, a.math_mode, cpu=(world == 1 and not a.no_cpu_baseline))
-
-    e2e = None
-    if rank == 0 and world == 1 and not a.no_e2e:
-        e2e = glow_tts_e2e_bench(dev, {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")})
-
-    xtts = None
-    if rank == 0 and world == 1 and not a.no_xtts:
-        xtts = xtts_decoder_bench(dev, a.math_mode)
-
-    vits = None
-    if rank == 0 and world == 1 and not a.no_vits:
-        vits = vits_bench(dev)
+    side = rank == 0 and world == 1
+    glow = glow_bench(dev, a.math_mode, cpu=not a.no_cpu_baseline) if side and not a.no_glow else None
+    e2e = (glow_tts_e2e_bench(dev, {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")})
+           if side and not a.no_e2e else None)
+    xtts = xtts_decoder_bench(dev, a.math_mode) if side and not a.no_xtts else None
+    vits = vits_bench(dev) if side and not a.no_vits else None
 
     if rank == 0:
-        rec = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": DTYPE[a.math_mode],
-            "math_mode": a.math_mode,
-            "data": "synthetic N(0,1) mel (seed=rank), synthetic variance-preserving HiFiGAN-v1 weights (seed 1234)",
-            "config": {
-                "workload": "HiFiGAN-v1 22.05kHz inference, [32,80,1024] mel per GPU (replicate pad 5), fp32",
-                "model": "HiFiGAN-v1 (hifigan_config.py generator_model_params)",
-                "global_batch": B * world,
-                "seq_len": T,
-                "parallelism": f"dp{world} (utterance sharding, no collectives)",
-            },
-            "rtf": rtf,
-            # samples of the unpadded mel (B * 256 * T), beside the padded numel above
-            "useful_samples_per_s": value * T / (T + 2 * pad),
-            "model_tflops": total_flops / (ms_per_step / 1e3) / 1e12,
-            "model_frac_fp32_peak": total_flops / (ms_per_step / 1e3) / 1e12 / FP32_PEAK_TFLOPS,
+        rec.update({
+            "model_tflops": total_flops / step_s / 1e12,
+            "model_frac_fp32_peak": total_flops / step_s / 1e12 / FP32_PEAK_TFLOPS,
             "roofline": {
                 "bound": "mfma",
                 "kernel": fam_name,
@@ -541,6 +699,7 @@ def main():
                 "flops_per_launch": per_launch_flops,
                 "avg_launch_ms": avg_ms,
                 **winograd_fields(fam_name, achieved, MODE_PEAK[a.math_mode]),
+                **busy,
             },
             "hbm_roofline_step": hbm,
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
@@ -551,12 +710,12 @@ def main():
             "xtts_decoder": xtts,
             "vits_waveform": vits,
             "accuracy_vs_fp64_oracle": acc,
-        }
-        if comm:
-            rec["comm"] = comm
+        })
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
 
 
 if __name__ == "__main__":

@@ -88,6 +88,9 @@ const char* tts_last_error(void);
 int tts_abi_version(void);
 /* Target the device code was built for ("gfx950"). */
 const char* tts_build_target(void);
+/* Provenance: "target=gfx950 src=<16 hex>", the first 16 hex digits of the sha256 of the
+ * library's sources (tts-3_amd/Makefile HASHED: sorted paths, contents concatenated) at build time. */
+const char* tts_build_info(void);
 
 /* ------------------------------------------------------------------------------------ */
 /* HiFiGAN generator                                                                     */

@@ -38,9 +38,20 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 108
+    assert N.lib().tts_abi_version() == 109
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
+
+
+def test_library_built_from_these_sources():
+    """Provenance: the loaded .so carries the hash of the sources in this tree (a stale or foreign
+    build fails here, before any GPU run uses it)."""
+    info = N.build_info()
+    assert info["target"] == "gfx950"
+    assert info["src"] == N.source_hash(), (
+        f"libtts_mi355x.so was built from other sources (src={info['src']}, tree={N.source_hash()}): "
+        "rebuild with make -C tts-3_amd")
+    assert len(info["lib_sha256"]) == 16
 
 
 def _cfg(**over):

@@ -11,8 +11,9 @@ from tts_amd.tts import Decoder
 pytestmark = pytest.mark.gpu
 GLOW = goldens("glow")
 # the reference's own fp32-vs-fp64 error on this flow is 2.9e-6 (12 flows, exp() of scales)
-GLOW_MAX_ABS = 1e-4
-GLOW_REL_RMS = 2e-5
+# (max); measured on MI355X: max 4.7e-6, rel-RMS 3.5e-7 (profiles/parity_errors_r03.jsonl)
+GLOW_MAX_ABS = 5e-5
+GLOW_REL_RMS = 5e-6
 
 
 def build(cfg, seed, device, math_mode="fp32"):

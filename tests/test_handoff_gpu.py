@@ -90,6 +90,21 @@ def test_wav_int16_nonfinite_matches_numpy(cuda_device):
             assert np.array_equal(out[b], handoff_ref.wav_int16(w[b, 0])), b
 
 
+def test_wav_int16_finite_overflow_matches_numpy(cuda_device):
+    """Finite samples whose scaled value reaches 2^31 (a NaN forces the scale to 32767 / 0.01):
+    x86 cvttss2si gives INT_MIN, whose low 16 bits are 0; just below 2^31 the value wraps."""
+    rng = np.random.default_rng(6)
+    w = (np.tanh(rng.standard_normal((2, 1, 1031))) * 0.5).astype(np.float32)
+    w[0, 0, 0] = np.nan
+    w[0, 0, 1:9] = [1000.0, -700.0, 655.0, 655.3, 656.0, -656.0, -655.3, 2.5e4]
+    w[1, 0, 3] = np.nan
+    w[1, 0, 100:103] = [-1e9, 654.9, 3.0e-3]
+    out = wav_to_int16(torch.from_numpy(w).to(cuda_device)).cpu().numpy()
+    with np.errstate(invalid="ignore", over="ignore"):
+        for b in range(2):
+            assert np.array_equal(out[b], handoff_ref.wav_int16(w[b, 0])), b
+
+
 @pytest.mark.parametrize("name,meta,arr", HRANGE, ids=[g[0] for g in HRANGE])
 def test_handoff_and_int16_vs_reference_functions(cuda_device, name, meta, arr):
     """Bit-exact against the reference's own AudioProcessor.normalize/denormalize and

@@ -48,4 +48,4 @@ def test_xtts_generator_vs_oracle_longer(cuda_device):
     g = torch.randn(3, 512, 1, generator=torch.Generator().manual_seed(2)) * 0.5
     out = d.waveform_decoder(x.to(cuda_device), g=g.to(cuda_device))
     ref = hifigan_ref.hifigan_forward(sd, x, pad=0, g=g, dtype=torch.float64, fold_dtype=torch.float64, **cfg)
-    assert_close_fp32(out.cpu(), ref, "xtts generator B=3 T=57")
+    assert_close_fp32(out.cpu(), ref, "xtts generator B=3 T=57", **tol("fp32"))

@@ -75,13 +75,13 @@ struct Conv1dArgs {
   int gate;
 };
 
-constexpr int kSplitGateTile = 20;
+constexpr int kSplitGateTile = 20;  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
 constexpr int kSplitWinoTile = 21;  // Winograd F(4,4), 128 rows x 64 tile columns (wino_kernel.hpp)
 // Winograd F(4,4) conv (kernels_conv_wino.hip): f16x3, Cout % 128 == 0, Cin % 16 == 0, K in {7, 11},
 // dilation 1/3/5, no mask / replicate padding / gate / ConvTranspose form
 bool wino_supported(int mode, int Cout, int Cin, int K, int dil);
 bool wino_enabled();
-void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s);  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
+void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s);
 // packed row rho of a gated in_layer -> original row: block j = rho / 128 holds tanh rows
 // [64j, 64j + 64) then sigmoid rows [H + 64j, H + 64j + 64) (H % 64 == 0)
 inline int gate_row_order(int rho, int H) {

@@ -180,8 +180,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
           for (int c = 0; c < 2; ++c) {
             const ConvTile t = conv_tile(mode, rb.convs[2 * m + c].tile);
             const int dil = rb.convs[2 * m].dil;
-            tiles_ok = tiles_ok && t.CK % 16 == 0 && ch % t.CK == 0 && ch % t.BM == 0;
-            rb.fused = rb.fused && t.CK == 16 && ceil_div(ch, t.BM) * t.BM == ch &&
+            // the fused kernels read the direct split packing: a Winograd-packed conv (7 *
+            // ceil(K/4) steps) must take the per-conv path
+            tiles_ok = tiles_ok && !t.WINO && t.CK % 16 == 0 && ch % t.CK == 0 && ch % t.BM == 0;
+            rb.fused = rb.fused && !t.WINO && t.CK == 16 && ceil_div(ch, t.BM) * t.BM == ch &&
                        (fuse_all ? resblock_pair_supported(mode, ch, k, dil) : resblock_pair_preferred(mode, ch, k, dil));
           }
         }

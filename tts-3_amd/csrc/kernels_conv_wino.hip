@@ -1,4 +1,5 @@
-// Winograd F(4,4) conv1d instances (wino_kernel.hpp) and the weight transform (host).
+// Winograd F(4,4) conv1d instances (wino_kernel.hpp, wino8_kernel.hpp); the host weight transform
+// pack_conv1d_wino is in pack.cpp.
 #include <cmath>
 #include <cstdlib>
 #include <vector>
@@ -19,31 +20,6 @@ bool wino_enabled() {
   return !(e && e[0] == '0');
 }
 
-
-// U_c[p][co][ci] = gc[p] * sum_k ga[p]^k w[co][ci][4c + k]  (fp64, taps >= K are zero), laid out as
-// the 7*NCH "taps" s = c*7 + p of an ordinary split-mode conv weight, then packed by
-// pack_conv1d_split (one power-of-two scale for all points: see split_device.hpp / DESIGN.md).
-int pack_conv1d_wino(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
-  const int nch = wino_chunks(K);
-  const int KS = kWinoPoints * nch;
-  std::vector<float> wt((size_t)Cout * Cin * KS);
-  for (int64_t oc = 0; oc < (int64_t)Cout * Cin; ++oc) {
-    const float* src = w + oc * K;
-    float* dst = wt.data() + oc * KS;
-    for (int c = 0; c < nch; ++c)
-      for (int p = 0; p < kWinoPoints; ++p) {
-        double acc = 0.0;
-        for (int k = 0; k < 4; ++k) {
-          const int tap = 4 * c + k;
-          if (tap >= K) continue;
-          const double g = p == 6 ? (k == 3 ? 1.0 : 0.0) : (p == 0 ? (k == 0 ? 1.0 : 0.0) : std::pow(kWinoGa[p], k));
-          acc += g * (double)src[tap];
-        }
-        dst[c * kWinoPoints + p] = (float)(kWinoGc[p] * acc);
-      }
-  }
-  return pack_conv1d_split(mode, wt.data(), Cout, Cin, KS, t, out);
-}
 
 void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
   TTS_REQUIRE(wino_supported(mode, a.Cout, a.Cin, K, a.dil), 3, "conv1d(winograd): unsupported configuration");

@@ -801,6 +801,8 @@ void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
     if constexpr (S::ROWB <= 80) {
       if (geo128 == 2) launch_res3_t<S, 128, 2>(a, B, s);
       else launch_res3_t<S, 128, 3>(a, B, s);
+    } else {
+      throw Error(3, "resblock3: 128 channels need a split scheme of at most 80-byte rows");
     }
   } else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
   else launch_res3_t<S, 64, 2>(a, B, s);

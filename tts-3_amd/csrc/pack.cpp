@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "wino_consts.hpp"
 
 namespace tts {
 
@@ -82,8 +83,12 @@ int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const 
   int e = 0;
   if (mode == MATH_FP32_F16X3) {
     float m = 0.f;
-    for (int64_t i = 0; i < (int64_t)Cout * Cin * K; ++i) m = std::max(m, std::fabs(w[i]));
-    TTS_REQUIRE(std::isfinite(m), 1, "conv weights contain inf/NaN");
+    bool finite = true;  // std::max(m, NaN) keeps m: test every element, not the running max
+    for (int64_t i = 0; i < (int64_t)Cout * Cin * K; ++i) {
+      finite = finite && std::isfinite(w[i]);
+      m = std::max(m, std::fabs(w[i]));
+    }
+    TTS_REQUIRE(finite, 1, "conv weights contain inf/NaN");
     if (m > 0.f) {
       int E;
       (void)std::frexp(m, &E);
@@ -152,6 +157,31 @@ void pack_convT(const float* w, int Cin, int Cout, int U, const ConvTile& t, flo
             const int ci = c * t.CK + cl;
             out[o++] = (co < Cout && ci < Cin) ? w[((int64_t)ci * Cout + co) * K + k] : 0.f;
           }
+}
+
+// U_c[p][co][ci] = gc[p] * sum_k ga[p]^k w[co][ci][4c + k]  (fp64, taps >= K are zero), laid out as
+// the 7*NCH "taps" s = c*7 + p of an ordinary split-mode conv weight, then packed by
+// pack_conv1d_split (one power-of-two scale for all points: see split_device.hpp / DESIGN.md).
+int pack_conv1d_wino(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out) {
+  const int nch = wino_chunks(K);
+  const int KS = kWinoPoints * nch;
+  std::vector<float> wt((size_t)Cout * Cin * KS);
+  for (int64_t oc = 0; oc < (int64_t)Cout * Cin; ++oc) {
+    const float* src = w + oc * K;
+    float* dst = wt.data() + oc * KS;
+    for (int c = 0; c < nch; ++c)
+      for (int p = 0; p < kWinoPoints; ++p) {
+        double acc = 0.0;
+        for (int k = 0; k < 4; ++k) {
+          const int tap = 4 * c + k;
+          if (tap >= K) continue;
+          const double g = p == 6 ? (k == 3 ? 1.0 : 0.0) : (p == 0 ? (k == 0 ? 1.0 : 0.0) : std::pow(kWinoGa[p], k));
+          acc += g * (double)src[tap];
+        }
+        dst[c * kWinoPoints + p] = (float)(kWinoGc[p] * acc);
+      }
+  }
+  return pack_conv1d_split(mode, wt.data(), Cout, Cin, KS, t, out);
 }
 
 }  // namespace tts

@@ -210,6 +210,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     job_load(0, j);
     job_finish(0, j);
   }
+  // raw(1) must have landed before the barrier: chunk 0's transform jobs read R[1] from its first
+  // step on.  No weight load is in flight yet, so this waits for the raw(1) DMA alone (it overlapped
+  // the chunk-0 transform above)
+  if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_sync();
   WSTAMP(2);
 

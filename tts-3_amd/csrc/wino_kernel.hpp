@@ -26,6 +26,7 @@
 #pragma once
 
 #include "split_device.hpp"
+#include "wino_consts.hpp"
 
 namespace tts {
 
@@ -34,12 +35,6 @@ namespace tts {
                        // 8 no MFMA, 16 no epilogue, 32 no input DMA (wino8)
 #endif
 
-constexpr int kWinoPoints = 7;
-constexpr int wino_chunks(int K) { return (K + 3) / 4; }
-// G[p][k] = gc[p] * ga[p]^k (k = 0..3); p = 6 (inf) only has k = 3.
-constexpr double kWinoGc[7] = {0.25, 1.0 / 6, 1.0 / 18, 1.0 / 72, 1.0 / 120, 32.0 / 45, 0.5};
-constexpr double kWinoGa[7] = {0.0, 1.0, -1.0, 2.0, -2.0, 0.5, 0.0};
-constexpr int kWinoBtShift = 5;  // max row sum of |BT| = 30 < 2^5: scale the input by 2^-(e+5)
 
 // V[p] = BT[p] . v for one channel (20 fp32 ops):
 //   BT = [[4,-8,-5,10,1,-2,0], [0,-4,4,9,-1,-2,0], [0,-4,12,-7,-3,2,0], [0,2,-3,-4,3,2,0],

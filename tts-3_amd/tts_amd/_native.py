@@ -140,6 +140,7 @@ SIGNATURES = {
     "tts_last_error": (c_char_p, []),
     "tts_abi_version": (c_int, []),
     "tts_build_target": (c_char_p, []),
+    "tts_build_info": (c_char_p, []),
     "tts_hifigan_num_weights": (c_int, [POINTER(TtsHifiganCfg)]),
     "tts_hifigan_weight_numel": (c_int64, [POINTER(TtsHifiganCfg), c_int]),
     "tts_hifigan_create": (c_int, [POINTER(TtsHifiganCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
@@ -229,6 +230,38 @@ SIGNATURES = {
 }
 
 _lib = None
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tts-3_amd/
+
+
+def source_hash(pkg_dir: str = _PKG_DIR) -> str:
+    """The src= stamp tts_build_info() should carry for the sources in ``pkg_dir`` (the Makefile's
+    HASHED list: SRCS, csrc/*.hpp, ../include/tts_mi355x.h and the Makefile, sorted by path)."""
+    import glob
+    import hashlib
+    import re
+
+    mk = open(os.path.join(pkg_dir, "Makefile")).read()
+    srcs = re.search(r"^SRCS := (.*)$", mk, re.M).group(1).split()
+    hdrs = [os.path.relpath(p, pkg_dir) for p in glob.glob(os.path.join(pkg_dir, "csrc", "*.hpp"))]
+    files = sorted(set(srcs + hdrs + ["../include/tts_mi355x.h", "Makefile"]))
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(pkg_dir, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """Provenance of the loaded library: its stamped source hash and the file's own sha256."""
+    import hashlib
+
+    info = lib().tts_build_info().decode()
+    fields = dict(kv.split("=", 1) for kv in info.split())
+    with open(LIB_PATH, "rb") as fh:
+        fields["lib_sha256"] = hashlib.sha256(fh.read()).hexdigest()[:16]
+    fields["lib_path"] = LIB_PATH
+    return fields
 
 
 class NativeError(RuntimeError):
