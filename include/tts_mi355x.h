@@ -177,7 +177,8 @@ typedef struct TtsGlowDecoderCfg {
   int num_splits;          /* 4 */
   int num_squeeze;         /* 2 */
   int sigmoid_scale;       /* 0 */
-  int c_in_channels;       /* 0 (speaker conditioning not implemented: must be 0) */
+  int c_in_channels;       /* 0 = unconditioned; > 0: speaker vector size, every WN gets a cond_layer
+                              (wavenet.py:64-66, :98-107) */
   int math_mode;           /* TTS_MATH_FP32 (default), _X6, _F16X3 or TTS_MATH_BF16 */
 } TtsGlowDecoderCfg;
 
@@ -185,6 +186,7 @@ typedef struct TtsGlowDecoderCfg {
  *   actnorm.logs [C2], actnorm.bias [C2]                          (C2 = in*num_squeeze)
  *   invconv.weight_inv [S][S]  (torch.inverse(weight), glow.py:139-141)
  *   coupling.start.weight [H][C2/2] (weight-norm folded), coupling.start.bias [H]
+ *   if c_in_channels: wn.cond_layer.weight [2*H*L][c_in] (weight-norm folded), bias [2*H*L]
  *   for l < L: wn.in_layers.l.weight [2H][H][k], wn.in_layers.l.bias [2H]
  *              wn.res_skip_layers.l.weight [l<L-1 ? 2H : H][H], bias
  *   coupling.end.weight [C2][H], coupling.end.bias [C2] */
@@ -193,14 +195,15 @@ int64_t tts_glow_decoder_weight_numel(const TtsGlowDecoderCfg* cfg, int idx);
 int tts_glow_decoder_create(const TtsGlowDecoderCfg* cfg, const float* const* host_weights,
                             int device, void** handle);
 int tts_glow_decoder_destroy(void* handle);
-/* y[B][C][T'] = Decoder.forward(x, x_mask, reverse=reverse)[0] with T' = T rounded down to a
- * multiple of num_squeeze (decoder.py:19); d_mask is [B][1][T] (0/1).  Only reverse = 1 is
- * implemented (the inference direction, glow_tts.py:363). */
-int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, int B, int C,
-                             int T, int reverse, float* d_y, void* hip_stream);
+/* y[B][C][T'] = Decoder.forward(x, x_mask, g, reverse=reverse)[0] with T' = T rounded down to a
+ * multiple of num_squeeze (decoder.py:19); d_mask is [B][1][T] (0/1); d_g is the speaker vector
+ * [B][c_in_channels] (the reference's g [B][c_in][1], decoder.py:113), NULL when c_in_channels == 0.
+ * Only reverse = 1 is implemented (the inference direction, glow_tts.py:363). */
+int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
+                             int C, int T, int reverse, float* d_y, void* hip_stream);
 /* Same with a hipEvent pair around every launch (synchronises; see tts_hifigan_forward_profiled). */
-int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, int B, int C,
-                                      int T, int reverse, float* d_y, void* hip_stream,
+int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                                      int B, int C, int T, int reverse, float* d_y, void* hip_stream,
                                       TtsLaunchRecord* records, int max_records, int* n_records);
 
 /* ------------------------------------------------------------------------------------ */

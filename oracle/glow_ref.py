@@ -11,7 +11,8 @@ CPU restatement of the Glow-TTS decoder flow (reverse direction, the inference p
   .permute(0,1,3,2,4), 1x1 conv2d with W^-1 (torch.inverse, :123/:140), regroup back, * mask
 * ``glow.py:201-230``  CouplingBlock reverse: h = start(x0)*mask; WN; out = end(h);
   t = out[:C/2], s = out[C/2:]; z1 = (x1 - t) * exp(-s) * mask; cat(x0, z1)
-* ``TTS/tts/layers/generic/wavenet.py:94-115`` (+ the fused gate :6-13, g = 0)
+* ``TTS/tts/layers/generic/wavenet.py:94-115`` (+ the fused gate :6-13): g_l = rows
+  [2Hl, 2H(l+1)) of cond_layer(g) (:98-107, weight norm folded by store_inverse :117-123), or 0
 
 Pinned against golden vectors of the reference module (tests/golden/make_goldens.py).
 """
@@ -41,12 +42,16 @@ def unsqueeze(x, x_mask, num_sqz=2):
     return x_unsqz * x_mask, x_mask
 
 
-def _wn(w, h, mask, L, H, kernel_size, dilation_rate, pre):
+def _wn(w, h, mask, L, H, kernel_size, dilation_rate, pre, g=None):
     output = torch.zeros_like(h)
+    if g is not None:
+        g = F.conv1d(g, w[f"{pre}.wn.cond_layer.weight"], w[f"{pre}.wn.cond_layer.bias"])
     for i in range(L):
         d = dilation_rate**i
         x_in = F.conv1d(h, w[f"{pre}.wn.in_layers.{i}.weight"], w[f"{pre}.wn.in_layers.{i}.bias"],
                         dilation=d, padding=int((kernel_size * d - d) / 2))
+        if g is not None:
+            x_in = x_in + g[:, i * 2 * H:(i + 1) * 2 * H, :]
         acts = torch.tanh(x_in[:, :H]) * torch.sigmoid(x_in[:, H:])
         rs = F.conv1d(acts, w[f"{pre}.wn.res_skip_layers.{i}.weight"], w[f"{pre}.wn.res_skip_layers.{i}.bias"])
         if i < L - 1:
@@ -72,14 +77,18 @@ def glow_decoder_reverse(
     sigmoid_scale: bool = False,
     dtype=torch.float64,
     fold_dtype=torch.float32,
+    g: torch.Tensor = None,
     **_unused,
 ):
+    """Decoder.forward(x, x_mask, g, reverse=True)[0]; g: speaker vector [B, c_in, 1] or None."""
     # store_inverse (glow.py:232-233) folds the WN layers' weight norm at load (fp32), but
     # CouplingBlock.start keeps its parametrization, so it is evaluated in the run dtype.
     w = fold_weight_norm({k: v for k, v in sd.items() if ".start." not in k}, dtype, fold_dtype)
     w.update(fold_weight_norm({k: v for k, v in sd.items() if ".start." in k}, dtype, dtype))
     x = x.to(dtype)
     x_mask = x_mask.to(dtype)
+    if g is not None:
+        g = g.to(dtype)
     if num_squeeze > 1:
         x, x_mask = squeeze(x, x_mask, num_squeeze)
     C2 = x.size(1)
@@ -91,7 +100,7 @@ def glow_decoder_reverse(
         # CouplingBlock reverse (glow.py:210-230)
         x0, x1 = x[:, : C2 // 2], x[:, C2 // 2 :]
         h = F.conv1d(x0, w[f"{pre}.start.weight"], w[f"{pre}.start.bias"]) * x_mask
-        h = _wn(w, h, x_mask, num_coupling_layers, H, kernel_size, dilation_rate, pre)
+        h = _wn(w, h, x_mask, num_coupling_layers, H, kernel_size, dilation_rate, pre, g)
         out = F.conv1d(h, w[f"{pre}.end.weight"], w[f"{pre}.end.bias"])
         t, s = out[:, : C2 // 2], out[:, C2 // 2 :]
         if sigmoid_scale:

@@ -4,6 +4,7 @@ Run in the development container only (it imports /root/reference, which does no
 the GPU box):   python tests/golden/make_goldens.py        (HiFiGAN + Glow fixtures)
                 python tests/golden/make_goldens.py vits   (VITS flow fixtures)
                 python tests/golden/make_goldens.py glow_tts (Glow-TTS encoder + inference glue)
+                python tests/golden/make_goldens.py glow_cond (speaker-conditioned Glow decoder)
 
 Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
 but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
@@ -218,7 +219,7 @@ def glow_case(Decoder, name, cfg, seed, B, T, lengths, x_seed):
         in_channels=cfg["in_channels"], hidden_channels=cfg["hidden_channels"], kernel_size=cfg["kernel_size"],
         dilation_rate=cfg["dilation_rate"], num_flow_blocks=cfg["num_flow_blocks"],
         num_coupling_layers=cfg["num_coupling_layers"], dropout_p=0.05, num_splits=cfg["num_splits"],
-        num_squeeze=cfg["num_squeeze"], sigmoid_scale=False, c_in_channels=0,
+        num_squeeze=cfg["num_squeeze"], sigmoid_scale=False, c_in_channels=cfg.get("c_in_channels", 0),
     )
     sd = synthetic.glow_decoder_state_dict(**cfg, seed=seed)
     ref.load_state_dict(sd)
@@ -226,18 +227,22 @@ def glow_case(Decoder, name, cfg, seed, B, T, lengths, x_seed):
     ref.store_inverse()  # glow_tts.py:519-520, :529 (eval load)
     gen = torch.Generator().manual_seed(x_seed)
     x = torch.randn(B, cfg["in_channels"], T, generator=gen)
+    c_in = cfg.get("c_in_channels", 0)
+    g = torch.randn(B, c_in, 1, generator=gen) if c_in else None  # speaker vector (decoder.py:113)
     lengths_t = torch.tensor(lengths)
     mask = (torch.arange(T)[None, :] < lengths_t[:, None]).float().unsqueeze(1)
     with torch.no_grad():
-        y32, _ = ref(x, mask, reverse=True)
+        y32, _ = ref(x, mask, g=g, reverse=True)
         ref64 = ref.double()
-        y64, _ = ref64(x.double(), mask.double(), reverse=True)
+        g64 = g.double() if g is not None else None
+        y64, _ = ref64(x.double(), mask.double(), g=g64, reverse=True)
         # round trip through the reference's own forward direction
-        z64, logdet = ref64(y64, mask.double()[:, :, : y64.size(2)], reverse=False)
+        z64, logdet = ref64(y64, mask.double()[:, :, : y64.size(2)], g=g64, reverse=False)
     meta = dict(kind="glow", config=cfg, seed=seed, x_seed=x_seed, B=B, T=T, lengths=lengths)
     path = os.path.join(HERE, f"{name}.npz")
+    extra = {"g": g.numpy()} if g is not None else {}
     np.savez_compressed(path, meta=json.dumps(meta), x=x.numpy(), mask=mask.numpy(), out_ref_fp32=y32.numpy(),
-                        out_ref_fp64=y64.numpy(), roundtrip_fp64=z64.numpy(), logdet_fp64=logdet.numpy())
+                        out_ref_fp64=y64.numpy(), roundtrip_fp64=z64.numpy(), logdet_fp64=logdet.numpy(), **extra)
     print(f"wrote {path}: out {tuple(y32.shape)} std {y32.std():.4f} "
           f"max|fp32-fp64| {np.abs(y32.numpy() - y64.numpy()).max():.2e}")
 
@@ -281,6 +286,8 @@ def main():
         return main_handoff()
     if len(sys.argv) > 1 and sys.argv[1] == "xtts":
         return main_xtts()
+    if len(sys.argv) > 1 and sys.argv[1] == "glow_cond":
+        return main_glow_cond()
     HifiganGenerator, Decoder = import_reference()
     v1 = dict(in_channels=80, out_channels=1, resblock_type="1",
               resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
@@ -310,6 +317,15 @@ def main():
                 num_coupling_layers=4, num_splits=4, num_squeeze=2)
     glow_case(Decoder, "glow_decoder_b2_t64", glow, seed=4321, B=2, T=64, lengths=[64, 41], x_seed=21)
     glow_case(Decoder, "glow_decoder_b3_t33", glow, seed=4322, B=3, T=33, lengths=[33, 20, 1], x_seed=22)
+
+
+def main_glow_cond():
+    _, Decoder = import_reference()
+    # G3b: multi-speaker Glow-TTS decoder (c_in_channels > 0: every WN's cond_layer, wavenet.py:64-66,
+    # :98-107), ragged mask with an odd length
+    glow = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+                num_coupling_layers=4, num_splits=4, num_squeeze=2, c_in_channels=24)
+    glow_case(Decoder, "glow_decoder_cond_b3_t37", glow, seed=4323, B=3, T=37, lengths=[37, 22, 5], x_seed=23)
 
 
 def main_vits():

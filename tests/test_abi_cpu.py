@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 109
+    assert N.lib().tts_abi_version() == 110
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -168,12 +168,33 @@ def test_glow_decoder_surface():
         d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), reverse=False)
 
 
+def test_glow_decoder_speaker_surface():
+    """c_in_channels > 0: the reference key set (every WN's cond_layer, weight-normed) loads strictly
+    and the weight inventory lines up with the C-ABI's."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=3,
+               num_coupling_layers=4)
+    d = Decoder(**cfg, num_splits=4, num_squeeze=2, c_in_channels=24)
+    sd = synthetic.glow_decoder_state_dict(**cfg, c_in_channels=24, seed=8)
+    d.load_state_dict(sd)
+    assert "flows.2.wn.cond_layer.parametrizations.weight.original1" in sd
+    d.store_inverse()
+    ws = d._weight_list()
+    n = N.lib().tts_glow_decoder_num_weights(ctypes.byref(d._cfg))
+    assert n == len(ws) == 3 * 25
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_decoder_weight_numel(ctypes.byref(d._cfg), i) == w.size
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), g=torch.zeros(1, 24, 1), reverse=True)
+
+
 def test_glow_config_validation():
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 3, 2, 0, 0)
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
     assert b"num_splits" in N.lib().tts_last_error()
-    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)
-    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)  # speaker-conditioned: + cond_layer w, b per flow
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 25
+    c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, -1)
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, N.MATH_MODES["f16x3"])
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 23  # f16x3 accepted (23 tensors per flow)
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, 9)

@@ -19,7 +19,8 @@ GLOW_REL_RMS = 5e-6
 def build(cfg, seed, device, math_mode="fp32"):
     d = Decoder(cfg["in_channels"], cfg["hidden_channels"], cfg["kernel_size"], cfg["dilation_rate"],
                 cfg["num_flow_blocks"], cfg["num_coupling_layers"], dropout_p=0.05,
-                num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"], math_mode=math_mode)
+                num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"],
+                c_in_channels=cfg.get("c_in_channels", 0), math_mode=math_mode)
     d.load_state_dict(synthetic.glow_decoder_state_dict(**cfg, seed=seed))
     d.eval()
     d.store_inverse()
@@ -32,7 +33,8 @@ def test_glow_reverse_vs_reference(cuda_device, name, meta, arr, mode):
     d = build(meta["config"], meta["seed"], cuda_device, mode)
     x = torch.from_numpy(arr["x"]).to(cuda_device)
     m = torch.from_numpy(arr["mask"]).to(cuda_device)
-    y, logdet = d(x, m, reverse=True)
+    g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None  # multi-speaker (c_in > 0)
+    y, logdet = d(x, m, g=g, reverse=True)
     assert logdet is None
     if mode == "bf16":
         assert_close_fp32(y.cpu(), arr["out_ref_fp64"], name, BF16_MAX_ABS, BF16_REL_RMS)
@@ -104,4 +106,46 @@ def test_glow_x0_statistics_match_prepass(cuda_device, monkeypatch):
         outs.append(d(x, m, reverse=True)[0])
         names.append([r["name"] for r in d.profile(x, m)[1]])
     assert names[0].count("glow_amax_x0") == 4 and names[1].count("glow_amax_x0") == 1
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3", "bf16"])
+def test_glow_speaker_conditioned_vs_oracle(cuda_device, mode):
+    """Multi-speaker decoder (c_in_channels > 0, decoder.py:113 with g): every flow's WN projects g
+    with its cond_layer and adds rows [2Hl, 2H(l+1)) to in_layer l (wavenet.py:98-107).  Longer and
+    ragged against the fp64 oracle; the same utterance alone is bit-identical (batch invariance)."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2, c_in_channels=256)
+    d = build(cfg, 57, cuda_device, mode)
+    gen = torch.Generator().manual_seed(58)
+    B, T = 4, 301
+    x = torch.randn(B, 80, T, generator=gen)
+    g = torch.randn(B, 256, 1, generator=gen)
+    m = (torch.arange(T)[None] < torch.tensor([301, 300, 128, 3])[:, None]).float().unsqueeze(1)
+    y, _ = d(x.to(cuda_device), m.to(cuda_device), g=g.to(cuda_device), reverse=True)
+    ref = glow_ref.glow_decoder_reverse(synthetic.glow_decoder_state_dict(**cfg, seed=57), x, m, g=g, **cfg)
+    if mode == "bf16":
+        assert_close_fp32(y.cpu(), ref, "glow cond (bf16)", BF16_MAX_ABS, BF16_REL_RMS)
+    else:
+        assert_close_fp32(y.cpu(), ref, f"glow cond ({mode})", GLOW_MAX_ABS, GLOW_REL_RMS)
+    y2, _ = d(x[2:3].to(cuda_device), m[2:3].to(cuda_device), g=g[2:3].to(cuda_device), reverse=True)
+    assert torch.equal(y2[0], y[2])
+    with pytest.raises(ValueError):
+        d(x.to(cuda_device), m.to(cuda_device), reverse=True)  # conditioned decoder without g
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3"])
+def test_glow_speaker_gate_fusion_bitwise(cuda_device, mode, monkeypatch):
+    """The speaker term g_l rides in the fused gate epilogue (cvec, original row order) exactly as in
+    the separate in_layer + gate launches."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=2,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2, c_in_channels=16)
+    gen = torch.Generator().manual_seed(19)
+    x = torch.randn(2, 80, 211, generator=gen).to(cuda_device)
+    g = torch.randn(2, 16, 1, generator=gen).to(cuda_device)
+    m = (torch.arange(211)[None] < torch.tensor([211, 90])[:, None]).float().unsqueeze(1).to(cuda_device)
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_FLOW_GATE", fused)
+        outs.append(build(cfg, 29, cuda_device, mode)(x, m, g=g, reverse=True)[0])
     assert torch.equal(outs[0], outs[1])

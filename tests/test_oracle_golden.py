@@ -62,12 +62,13 @@ def test_hifigan_stage_intermediates():
 def test_glow_oracle_matches_reference(name, meta, arr):
     cfg = meta["config"]
     sd = synthetic.glow_decoder_state_dict(**cfg, seed=meta["seed"])
+    g = torch.from_numpy(arr["g"]) if "g" in arr else None  # speaker vector (c_in_channels > 0)
     out = glow_ref.glow_decoder_reverse(sd, torch.from_numpy(arr["x"]), torch.from_numpy(arr["mask"]),
-                                        dtype=torch.float64, **cfg)
+                                        dtype=torch.float64, g=g, **cfg)
     assert out.shape == arr["out_ref_fp64"].shape
     assert max_abs(out.numpy(), arr["out_ref_fp64"]) < 1e-10
     out32 = glow_ref.glow_decoder_reverse(sd, torch.from_numpy(arr["x"]), torch.from_numpy(arr["mask"]),
-                                          dtype=torch.float32, **cfg)
+                                          dtype=torch.float32, g=g, **cfg)
     assert max_abs(out32.numpy(), arr["out_ref_fp32"]) < 1e-5
 
 

@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 109; }
+int tts_abi_version(void) { return 110; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -326,18 +326,18 @@ int tts_glow_decoder_destroy(void* handle) {
   return guarded([&] { delete static_cast<tts::GlowDecoder*>(handle); });
 }
 
-int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, int B, int C,
-                             int T, int reverse, float* d_y, void* hip_stream) {
+int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
+                             int C, int T, int reverse, float* d_y, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
     TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
-    static_cast<tts::GlowDecoder*>(handle)->reverse(d_x, d_mask, B, C, T, d_y,
+    static_cast<tts::GlowDecoder*>(handle)->reverse(d_x, d_mask, d_g, B, C, T, d_y,
                                                     static_cast<hipStream_t>(hip_stream));
   });
 }
 
-int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, int B, int C,
-                                      int T, int reverse, float* d_y, void* hip_stream,
+int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                                      int B, int C, int T, int reverse, float* d_y, void* hip_stream,
                                       TtsLaunchRecord* records, int max_records, int* n_records) {
   return guarded([&] {
     TTS_REQUIRE(handle && n_records, 1, "NULL argument");
@@ -347,7 +347,7 @@ int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const floa
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->reverse(d_x, d_mask, B, C, T, d_y, s, &prof);
+      h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);

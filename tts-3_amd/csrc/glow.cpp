@@ -54,6 +54,10 @@ std::vector<int64_t> glow_weight_shapes(const TtsGlowDecoderCfg& c) {
     n.push_back((int64_t)S * S);          // invconv.weight_inv
     n.push_back((int64_t)H * (C2 / 2));   // start.weight
     n.push_back(H);                       // start.bias
+    if (c.c_in_channels > 0) {            // wn.cond_layer (weight norm folded), wavenet.py:64-66
+      n.push_back((int64_t)2 * H * c.num_coupling_layers * c.c_in_channels);
+      n.push_back((int64_t)2 * H * c.num_coupling_layers);
+    }
     for (int l = 0; l < c.num_coupling_layers; ++l) {
       n.push_back((int64_t)2 * H * H * c.kernel_size);
       n.push_back(2 * H);
@@ -85,7 +89,7 @@ void glow_validate(const TtsGlowDecoderCfg& c) {
     TTS_REQUIRE((c.kernel_size - 1) * d <= 96, 3, "(kernel_size-1)*dilation above 96 is not implemented");
     d *= c.dilation_rate;
   }
-  TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned Glow decoder (c_in_channels > 0) not implemented");
+  TTS_REQUIRE(c.c_in_channels >= 0, 1, "c_in_channels must be >= 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
 }
 
@@ -146,6 +150,11 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
     put(hw[wi], C2, &F.logs); put(hw[wi + 1], C2, &F.bias); put(hw[wi + 2], (size_t)S * S, &F.winv);
     wi += 3;
     put_conv(F.start, hw[wi], hw[wi + 1], C2 / 2, H, 1, 1); wi += 2;
+    if (cfg_.c_in_channels > 0) {  // cond_layer stays fp32 [2HL][c_in] (launch_cond_vec)
+      put(hw[wi], (size_t)2 * H * L * cfg_.c_in_channels, &F.cond_w);
+      put(hw[wi + 1], (size_t)2 * H * L, &F.cond_b);
+      wi += 2;
+    }
     F.in_layers.resize(L); F.res_skip.resize(L);
     int d = 1;
     for (int l = 0; l < L; ++l) {
@@ -178,24 +187,27 @@ void GlowDecoder::reserve(int B, int Th) {
   const int C2 = cfg_.in_channels * cfg_.num_squeeze;
   const int H = cfg_.hidden_channels;
   const size_t plane = (size_t)B * Th;
-  // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1; f16x3: max-abs slot groups
-  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 8 * sizeof(float) +
-                      amax_floats(B) * sizeof(float);
+  // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1; cond vectors [B][2HL]; f16x3: max-abs
+  // slot groups
+  const size_t cond = cfg_.c_in_channels > 0 ? (size_t)B * 2 * H * cfg_.num_coupling_layers + 64 : 0;
+  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 9 * sizeof(float) +
+                      (cond + amax_floats(B)) * sizeof(float);
   if (need <= ws_bytes_) return;
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
   ws_bytes_ = need;
 }
 
-void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s,
-                          Profiler* prof) {
+void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int B, int C, int T, float* y,
+                          hipStream_t s, Profiler* prof) {
   TTS_REQUIRE(x && mask && y, 1, "NULL input/output pointer");
+  TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1, 1, "batch must be >= 1");
   TTS_REQUIRE(C == cfg_.in_channels, 1, "channel count does not match the decoder");
   const int nsq = cfg_.num_squeeze;
   const int Th = T / nsq;
   TTS_REQUIRE(Th >= 1, 1, "T too short for num_squeeze");
-  DeviceGuard g(device_);
+  DeviceGuard dg(device_);
   reserve(B, Th);
   const int C2 = C * nsq;
   const int H = cfg_.hidden_channels;
@@ -211,6 +223,8 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   float* skip = p; p += al(plane * H);
   float* out = p; p += al(plane * C2);
   float* msq = p; p += al(plane);
+  float* cvec = nullptr;  // cond_layer(g) of the current flow, [B][2HL] (wavenet.py:98-99)
+  if (cfg_.c_in_channels > 0) { cvec = p; p += al((size_t)B * 2 * H * L); }
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
   unsigned* amax = h3 ? reinterpret_cast<unsigned*>(p) : nullptr;
   const int ng = 2 * L + 2;
@@ -229,10 +243,11 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   }
 
   auto conv = [&](const char* name, const Conv& cv, const float* in, int64_t in_bstride, float* o, const float* m,
-                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
+                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr, const float* cv_vec = nullptr) {
     Conv1dArgs a{};
     a.gate = cv.gated ? cv.Cout / 2 : 0;
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = o; a.mask = m; a.x_bstride = in_bstride;
+    a.cvec = cv_vec; a.cvec_bstride = cv_vec ? (int64_t)2 * H * L : 0;
     a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = cv.w_exp;
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th;
     a.dil = cv.dil; a.pad = cv.dil * (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;
@@ -245,16 +260,21 @@ void GlowDecoder::reverse(const float* x, const float* mask, int B, int C, int T
   for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
     const Flow& F = flows_[f];
     const int fi = cfg_.num_flow_blocks - 1 - f;
+    if (cvec)  // g = cond_layer(g) (wavenet.py:98-99); every flow has its own cond_layer
+      run(prof, s, "glow_cond", 2.0 * B * 2 * H * L * cfg_.c_in_channels, 4.0 * B * 2 * H * L,
+          [&] { launch_cond_vec(g, F.cond_w, F.cond_b, cvec, B, cfg_.c_in_channels, 2 * H * L, s); });
     if (h3 && (fi == 0 || amax_prepass_))  // statistics of x_0 (the start conv's input); later flows: the previous tail
       run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
     conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq, slots(fi, 0), slots(fi, 1));
     for (int l = 0; l < L; ++l) {
+      // x_in = in_layers[l](h) + g_l  (wavenet.py:101-107; g_l = cond rows [2Hl, 2H(l+1)))
+      const float* gl = cvec ? cvec + (size_t)l * 2 * H : nullptr;
       if (F.in_layers[l].gated) {  // wavenet.py:101 + :108 in one launch, acts straight from the epilogue
-        conv("glow_wn_in_gate", F.in_layers[l], hb, 0, acts, nullptr, slots(fi, 1 + l), slots(fi, 1 + L + l));
+        conv("glow_wn_in_gate", F.in_layers[l], hb, 0, acts, nullptr, slots(fi, 1 + l), slots(fi, 1 + L + l), gl);
       } else {
-        conv("glow_wn_in", F.in_layers[l], hb, 0, xin, nullptr, slots(fi, 1 + l));  // wavenet.py:101
+        conv("glow_wn_in", F.in_layers[l], hb, 0, xin, nullptr, slots(fi, 1 + l), nullptr, gl);  // wavenet.py:101
         run(prof, s, "glow_gate", 0.0, 12.0 * P * H,
             [&] { launch_glow_gate(xin, acts, B, H, Th, s, slots(fi, 1 + L + l)); });  // :108
       }

@@ -62,7 +62,8 @@ class GlowDecoder {
   ~GlowDecoder();
   GlowDecoder(const GlowDecoder&) = delete;
   GlowDecoder& operator=(const GlowDecoder&) = delete;
-  void reverse(const float* x, const float* mask, int B, int C, int T, float* y, hipStream_t s,
+  // g: [B][c_in_channels] speaker vector (the reference's g [B][c_in][1]), NULL when c_in_channels == 0
+  void reverse(const float* x, const float* mask, const float* g, int B, int C, int T, float* y, hipStream_t s,
                Profiler* prof = nullptr);
   int device() const { return device_; }
 
@@ -77,6 +78,8 @@ class GlowDecoder {
     float* logs = nullptr;
     float* bias = nullptr;
     float* winv = nullptr;
+    float* cond_w = nullptr;  // wn.cond_layer [2HL][c_in] fp32 (c_in_channels > 0)
+    float* cond_b = nullptr;
     Conv start, end;
     std::vector<Conv> in_layers, res_skip;
   };

@@ -132,12 +132,15 @@ def glow_decoder_state_dict(
     num_splits: int = GLOW_TTS_DECODER["num_splits"],
     num_squeeze: int = GLOW_TTS_DECODER["num_squeeze"],
     seed: int = 4321,
+    c_in_channels: int = 0,
     **_unused,
 ) -> "OrderedDict[str, torch.Tensor]":
     """State dict of a Glow-TTS ``Decoder`` (decoder.py:68-111) with synthetic weights.
 
     ``end`` (zero-initialised in the reference, glow.py:194-196) and ActNorm are randomised too,
-    otherwise the reverse flow is an identity map and parity says nothing.
+    otherwise the reverse flow is an identity map and parity says nothing.  ``c_in_channels > 0``
+    adds every WN's ``cond_layer`` (wavenet.py:64-66), drawn after the flow's other weights so the
+    unconditioned stream (and every existing fixture) is unchanged.
     """
     rng = np.random.default_rng(seed)
     sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
@@ -170,6 +173,8 @@ def glow_decoder_state_dict(
         for l in range(num_coupling_layers):
             rsc = 2 * H if l < num_coupling_layers - 1 else H
             wn_conv(f"flows.{cb}.wn.res_skip_layers.{l}", rsc, H, 1, 1.0)
+        if c_in_channels > 0:
+            wn_conv(f"flows.{cb}.wn.cond_layer", 2 * H * num_coupling_layers, c_in_channels, 1, 1.0)
     return sd
 
 

@@ -3,10 +3,12 @@
 Mirrors ``TTS/tts/layers/glow_tts/decoder.py`` (Coqui TTS 0.22.0): same constructor
 (:68-81), same parameter tree (``flows.{3b}`` ActNorm ``logs``/``bias``, ``flows.{3b+1}``
 InvConvNear ``weight`` (+``weight_inv`` after ``store_inverse``), ``flows.{3b+2}`` CouplingBlock
-``start`` (weight-normed), ``end``, ``wn.in_layers.*`` / ``wn.res_skip_layers.*``), so reference
-checkpoints load unchanged.  ``forward(x, x_mask, g=None, reverse=True)`` returns
-``(y, None)`` like the reference (:113-137); the training direction (``reverse=False``,
-log-determinants) is out of scope and raises.
+``start`` (weight-normed), ``end``, ``wn.in_layers.*`` / ``wn.res_skip_layers.*``, and
+``wn.cond_layer`` when ``c_in_channels > 0``), so reference checkpoints load unchanged.
+``forward(x, x_mask, g=None, reverse=True)`` returns ``(y, None)`` like the reference (:113-137);
+``g`` ([B, c_in_channels, 1]) is the speaker vector every flow's WN projects with its own
+``cond_layer`` and adds to its in_layer outputs (wavenet.py:98-107).  The training direction
+(``reverse=False``, log-determinants) is out of scope and raises.
 
 The nn modules below only hold parameters.  Weight norm is folded with PyTorch's own
 ``_weight_norm`` and InvConvNear's inverse is ``torch.inverse(weight.float())`` exactly as
@@ -187,6 +189,8 @@ class Decoder(nn.Module):
             an, ic, cb = self.flows[3 * b], self.flows[3 * b + 1], self.flows[3 * b + 2]
             ws += [_t(an.logs).reshape(-1), _t(an.bias).reshape(-1), _t(ic.inverse_weight())]
             ws += [_w(cb.start), _t(cb.start.bias)]
+            if self.c_in_channels > 0:
+                ws += [_w(cb.wn.cond_layer).reshape(-1), _t(cb.wn.cond_layer.bias)]
             for l in range(self.num_coupling_layers):
                 ws += [_w(cb.wn.in_layers[l]), _t(cb.wn.in_layers[l].bias)]
                 ws += [_w(cb.wn.res_skip_layers[l]), _t(cb.wn.res_skip_layers[l].bias)]
@@ -238,11 +242,22 @@ class Decoder(nn.Module):
         return super()._apply(fn, *args, **kwargs)
 
     # ------------------------------------------------------------------ reference API
+    def _speaker(self, g: Optional[torch.Tensor], B: int, dev: torch.device) -> Optional[torch.Tensor]:
+        """g [B, c_in, 1] (or [B, c_in]) -> contiguous fp32 [B, c_in] on the device; None when unconditioned."""
+        if self.c_in_channels == 0:
+            if g is not None:
+                raise ValueError("g given to a Decoder built with c_in_channels=0 (it has no cond_layer)")
+            return None
+        if g is None:
+            raise ValueError(f"this Decoder is speaker-conditioned (c_in_channels={self.c_in_channels}): pass g")
+        g = g.to(device=dev, dtype=torch.float32).reshape(g.shape[0], -1).contiguous()
+        if g.shape != (B, self.c_in_channels):
+            raise ValueError(f"g has shape {tuple(g.shape)}, expected [{B}, {self.c_in_channels}, 1]")
+        return g
+
     def forward(self, x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None, reverse: bool = False):
         if not reverse:
             raise NotImplementedError("tts_amd Decoder implements the reverse (inference) flow only")
-        if g is not None:
-            raise NotImplementedError("speaker conditioning (g) is not implemented on the MI355X path")
         with torch.no_grad():
             h = self._native_handle()
             dev = self._device()
@@ -251,25 +266,28 @@ class Decoder(nn.Module):
             if x_mask is None:
                 x_mask = torch.ones(B, 1, T, device=dev)
             m = x_mask.to(device=dev, dtype=torch.float32).reshape(B, T).contiguous()
+            gv = self._speaker(g, B, dev)
             Tq = (T // self.num_squeeze) * self.num_squeeze if self.num_squeeze > 1 else T
             y = torch.empty(B, C, Tq, device=dev, dtype=torch.float32)
-            N.call("tts_glow_decoder_forward", h, N.ptr(x), N.ptr(m), B, C, T, 1, N.ptr(y), N.stream_ptr(dev))
+            N.call("tts_glow_decoder_forward", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1, N.ptr(y),
+                   N.stream_ptr(dev))
         return y, None
 
-    def profile(self, x: torch.Tensor, x_mask: torch.Tensor):
+    def profile(self, x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None):
         """One reverse pass with a hipEvent pair around every launch: (y, [{name, flops, bytes, ms}])."""
         h = self._native_handle()
         dev = self._device()
         x = x.to(device=dev, dtype=torch.float32).contiguous()
         B, C, T = x.shape
         m = x_mask.to(device=dev, dtype=torch.float32).reshape(B, T).contiguous()
+        gv = self._speaker(g, B, dev)
         Tq = (T // self.num_squeeze) * self.num_squeeze if self.num_squeeze > 1 else T
         y = torch.empty(B, C, Tq, device=dev)
         cap = 2048
         recs = (N.TtsLaunchRecord * cap)()
         n = ctypes.c_int(0)
-        N.call("tts_glow_decoder_forward_profiled", h, N.ptr(x), N.ptr(m), B, C, T, 1, N.ptr(y), N.stream_ptr(dev),
-               recs, cap, ctypes.byref(n))
+        N.call("tts_glow_decoder_forward_profiled", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1, N.ptr(y),
+               N.stream_ptr(dev), recs, cap, ctypes.byref(n))
         rows = [{"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
                 for i in range(min(n.value, cap))]
         return y, rows
