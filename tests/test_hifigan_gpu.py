@@ -397,3 +397,62 @@ def test_whole_block_fusion_matches_unfused(cuda_device, monkeypatch, mode):
         outs.append(g.inference(mel.to(cuda_device)).cpu())
         assert_close_fp32(outs[-1], ref, f"{mode} resblock3={policy}", **tol(mode))
     assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)
+
+
+def _padded_slice(mel, pad, a, b):
+    """Frames [a, b) of the replicate-padded mel (hifigan_generator.py:281), clamped indices."""
+    T = mel.shape[2]
+    idx = (torch.arange(a, b) - pad).clamp(0, T - 1)
+    return mel[:, :, idx]
+
+
+@pytest.mark.parametrize("mode", ["fp32", "f16x3", "bf16"])
+def test_windowed_forward_matches_plain(cuda_device, monkeypatch, mode):
+    """Long-utterance path at an ordinary length: TTS_MI355X_WINDOW_FRAMES forces 37-frame payloads
+    with the receptive-field halo on each side.  The payload samples of every window equal the
+    plain forward's (fp32: bit for bit, the same sums in the same order; the split modes take a
+    per-window power-of-two scale, so within the gates of the fp64 oracle)."""
+    sd = synthetic.hifigan_state_dict(seed=91, weight_norm=False)
+    mel = synthetic.mel(2, 150, seed=92)
+    outs = {}
+    for frames in ("0", "37"):
+        monkeypatch.setenv("TTS_MI355X_WINDOW_FRAMES", frames)
+        g = HifiganGenerator(**V1, math_mode=mode)
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs[frames] = g.inference(mel.to(cuda_device)).cpu()
+        if frames == "37":
+            names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+            assert names.count("mel_window") == 5  # ceil(160 / 37) windows
+    if mode == "fp32":
+        assert torch.equal(outs["0"], outs["37"])
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    assert_close_fp32(outs["37"], ref, f"windowed ({mode})", **tol(mode))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", ["f16x3", "fp32"])
+def test_long_utterance_beyond_plane_cap(cuda_device, mode):
+    """An utterance whose 128-channel plane passes 2 GiB (T' = 65540 padded frames > 65535, the
+    kernels' 32-bit range): windowed automatically.  Checked against the fp64 oracle on frame
+    ranges at the start, across the window seam and at the end (each oracle run sees its
+    range plus 32 frames of context: more than the 16-frame receptive field)."""
+    sd = synthetic.hifigan_state_dict(seed=93, weight_norm=False)
+    T, pad = 65530, 5
+    mel = synthetic.mel(1, T, seed=94)
+    g = HifiganGenerator(**V1, math_mode=mode)
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    y = g.inference(mel.to(cuda_device))
+    L = T + 2 * pad
+    assert y.shape == (1, 1, 256 * L)
+    assert torch.isfinite(y).all() and y.abs().max() <= 1.0
+    y = y.cpu()
+    ctx = 32
+    for a, b in [(0, 24), (65490, 65520), (L - 24, L)]:
+        lo, hi = max(0, a - ctx), min(L, b + ctx)
+        ref = hifigan_ref.hifigan_forward(sd, _padded_slice(mel, pad, lo, hi), pad=0, dtype=torch.float64, **V1)
+        ref = ref[:, :, 256 * (a - lo):256 * (b - lo)]
+        assert_close_fp32(y[:, :, 256 * a:256 * b], ref, f"long utterance frames [{a},{b}) ({mode})", **tol(mode))

@@ -157,6 +157,9 @@ int convT_tile_for(int Cout, int U);
 ConvTile convT_tile(int idx, int U);
 void launch_convT(const ConvTArgs& a, int B, int U, int tile_idx, hipStream_t s);
 void launch_conv_post(const PostArgs& a, int B, hipStream_t s);
+// out[b][c][t] = mel[b][c][clamp(w0 + t - pad, 0, T - 1)], t < W: one time window of the
+// replicate-padded mel (hifigan_generator.py:281) for the windowed long-utterance forward
+void launch_mel_window(const float* mel, int B, int C, int T, int pad, int64_t w0, int W, float* out, hipStream_t s);
 // cvec[b][co] = bc[co] + sum_i Wc[co][i] * g[b][i]   (cond_layer, hifigan_generator.py:228)
 void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
                      int C0, hipStream_t s);

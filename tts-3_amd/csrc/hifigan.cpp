@@ -4,6 +4,8 @@
 // on the caller's stream.
 #include "hifigan.hpp"
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -300,6 +302,7 @@ Hifigan::~Hifigan() {
   DeviceGuard g(device_);
   if (arena_) (void)hipFree(arena_);
   if (ws_) (void)hipFree(ws_);
+  if (win_) (void)hipFree(win_);
 }
 
 int64_t Hifigan::out_len(int T, int pad) const { return (int64_t)hop_ * (T + 2 * pad); }
@@ -333,19 +336,95 @@ int64_t Hifigan::cond_floats(int B) const {
   return n;
 }
 
-int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
-  const int64_t cond = cond_floats(B);
-  const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
-  return (4 * plane_floats(B, T, pad) + cond + amax) * (int64_t)sizeof(float);
+// ---------------------------------------------------------------------------------------
+// Time windows for long utterances
+// ---------------------------------------------------------------------------------------
+int Hifigan::window_halo() const {
+  // receptive-field radius of one output sample, in mel frames: conv_pre (k7), then per stage the
+  // polyphase ConvTranspose (taps x[m-1], x[m]: one input sample) and the widest MRF branch
+  // (ResBlock1: sum_m (k-1)/2 * (d_m + 1); ResBlock2: sum_m (k-1)/2 * d_m samples at the
+  // stage's rate), then conv_post (k7) at the output rate
+  double r = 3.0, rate = 1.0;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    r += 1.0 / rate;
+    rate *= cfg_.upsample_factors[i];
+    int widest = 0;
+    for (int j = 0; j < cfg_.num_kernels; ++j) {
+      const int h = (cfg_.resblock_kernel_sizes[j] - 1) / 2;
+      int w = 0;
+      for (int m = 0; m < (cfg_.resblock_type == 1 ? 3 : 2); ++m)
+        w += h * cfg_.resblock_dilation_sizes[j][m] + (cfg_.resblock_type == 1 ? h : 0);
+      widest = std::max(widest, w);
+    }
+    r += widest / rate;
+  }
+  r += 3.0 / rate;
+  return (int)std::ceil(r) + 2;
 }
 
-void Hifigan::reserve(int B, int T, int pad) {
-  const int64_t need = workspace_bytes(B, T, pad);
+int64_t Hifigan::max_window_frames() const {
+  // the kernels address one batch item's channel plane with 32-bit byte offsets: C * len < 2^29
+  int64_t cr = cfg_.upsample_initial_channel, rate = 1;
+  for (int i = 0; i < cfg_.num_upsamples; ++i) {
+    rate *= cfg_.upsample_factors[i];
+    cr = std::max(cr, (int64_t)(cfg_.upsample_initial_channel >> (i + 1)) * rate);
+  }
+  return ((int64_t(1) << 29) - 1) / cr;
+}
+
+int64_t Hifigan::window_payload() const {
+  // TTS_MI355X_WINDOW_FRAMES=<n> forces n-frame payloads (tests: windows at ordinary lengths)
+  const char* e = std::getenv("TTS_MI355X_WINDOW_FRAMES");
+  const int64_t cap = max_window_frames() - 2 * window_halo();
+  if (e && std::atoll(e) > 0) return std::min<int64_t>(std::atoll(e), cap);
+  return cap;
+}
+
+bool Hifigan::windowed(int64_t L) const {
+  const char* e = std::getenv("TTS_MI355X_WINDOW_FRAMES");
+  return L > max_window_frames() || (e && std::atoll(e) > 0 && L > std::atoll(e));
+}
+
+int64_t Hifigan::plain_workspace_bytes(int B, int64_t L) const {
+  const int64_t cond = cond_floats(B);
+  const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
+  return (4 * plane_floats(B, (int)L, 0) + cond + amax) * (int64_t)sizeof(float);
+}
+
+int64_t Hifigan::window_buffer_bytes(int B, int64_t W) const {
+  return ((((int64_t)B * cfg_.in_channels * W + 63) / 64) * 64 + (int64_t)B * hop_ * W) * (int64_t)sizeof(float);
+}
+
+int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
+  const int64_t L = (int64_t)T + 2 * pad;
+  if (!windowed(L)) return plain_workspace_bytes(B, L);
+  const int64_t W = std::min<int64_t>(L, window_payload() + 2 * window_halo());
+  return plain_workspace_bytes(B, W) + window_buffer_bytes(B, W);
+}
+
+void Hifigan::reserve_plain(int B, int64_t L) {
+  const int64_t need = plain_workspace_bytes(B, L);
   if ((size_t)need <= ws_bytes_) return;
   DeviceGuard g(device_);
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
   ws_bytes_ = need;
+}
+
+void Hifigan::reserve(int B, int T, int pad) {
+  const int64_t L = (int64_t)T + 2 * pad;
+  if (!windowed(L)) {
+    reserve_plain(B, L);
+    return;
+  }
+  const int64_t W = std::min<int64_t>(L, window_payload() + 2 * window_halo());
+  reserve_plain(B, W);
+  const int64_t need = window_buffer_bytes(B, W);
+  if ((size_t)need <= win_bytes_) return;
+  DeviceGuard g(device_);
+  if (win_) { TTS_HIP_CHECK(hipFree(win_)); win_ = nullptr; win_bytes_ = 0; }
+  if (hipMalloc(&win_, need) != hipSuccess) throw Error(4, "hipMalloc(window buffers) failed");
+  win_bytes_ = need;
 }
 
 void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const float* gvec, float* wav,
@@ -357,8 +436,38 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   TTS_REQUIRE(T >= 1, 1, "T must be >= 1");
   TTS_REQUIRE(pad >= 0, 1, "pad must be >= 0");
   TTS_REQUIRE(cfg_.cond_channels == 0 || gvec != nullptr, 1, "cond_channels > 0 requires g");
-  DeviceGuard g(device_);
+  const int64_t L = (int64_t)T + 2 * pad;
+  if (!windowed(L)) {
+    forward_plain(mel, B, C, T, pad, gvec, wav, s, prof);
+    return;
+  }
+  DeviceGuard dg(device_);
   reserve(B, T, pad);
+  const int h = window_halo();
+  const int64_t P = window_payload();
+  TTS_REQUIRE(P >= 1, 3, "window payload must be >= 1 frame");
+  const int64_t Wmax = std::min<int64_t>(L, P + 2 * h);
+  float* melw = win_;
+  float* outw = win_ + (((int64_t)B * C * Wmax + 63) / 64) * 64;
+  for (int64_t s0 = 0; s0 < L; s0 += P) {
+    const int64_t s1 = std::min(L, s0 + P);
+    const int64_t w0 = std::max<int64_t>(0, s0 - h), w1 = std::min(L, s1 + h);
+    const int W = (int)(w1 - w0);
+    // melw[b][c][t] = replicate_pad(mel)[b][c][w0 + t]  (hifigan_generator.py:281)
+    run(prof, s, "mel_window", 0.0, 8.0 * B * C * (double)W,
+        [&] { launch_mel_window(mel, B, C, T, pad, w0, W, melw, s); });
+    forward_plain(melw, B, C, W, 0, gvec, outw, s, prof);
+    // the payload's samples: outw[b][hop*(s0-w0) ...) -> wav[b][hop*s0 ...)
+    TTS_HIP_CHECK(hipMemcpy2DAsync(wav + hop_ * s0, sizeof(float) * hop_ * L, outw + hop_ * (s0 - w0),
+                                   sizeof(float) * hop_ * W, sizeof(float) * hop_ * (s1 - s0), B,
+                                   hipMemcpyDeviceToDevice, s));
+  }
+}
+
+void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, const float* gvec, float* wav,
+                            hipStream_t s, Profiler* prof) {
+  DeviceGuard g(device_);
+  reserve_plain(B, (int64_t)T + 2 * pad);
 
   const int64_t plane = plane_floats(B, T, pad);
   float* bufZ = ws_;              // conv_pre output, then the MRF sum of each stage

@@ -67,9 +67,17 @@ class Hifigan {
   int64_t out_len(int T, int pad) const;
   int64_t workspace_bytes(int B, int T, int pad) const;
   void reserve(int B, int T, int pad);
+  // Utterances whose padded length L = T + 2 pad exceeds one window (a channel plane of a batch
+  // item would pass 2 GiB, the kernels' 32-bit buffer range, or TTS_MI355X_WINDOW_FRAMES is set)
+  // run as overlapping time windows: payload [s0, s1) with window_halo() frames of context on
+  // each side (>= the generator's receptive-field radius), each window through the plain
+  // forward on a gathered copy of the replicate-padded mel, the payload's samples copied out.
   void forward(const float* mel, int B, int C, int T, int pad, const float* g, float* wav,
                hipStream_t s, Profiler* prof);
   int device() const { return device_; }
+  int window_halo() const;        // receptive-field radius in mel frames, rounded up, + 2
+  int64_t max_window_frames() const;  // largest window whose every channel plane stays < 2 GiB
+  int64_t window_payload() const;     // payload frames per window
 
  private:
   struct ConvLayer {
@@ -96,6 +104,12 @@ class Hifigan {
     bool fused3 = false;           // type 1, kernel 3: the whole block in one launch (resblock3)
   };
 
+  void forward_plain(const float* mel, int B, int C, int T, int pad, const float* g, float* wav, hipStream_t s,
+                     Profiler* prof);
+  bool windowed(int64_t L) const;
+  int64_t plain_workspace_bytes(int B, int64_t L) const;
+  int64_t window_buffer_bytes(int B, int64_t W) const;
+  void reserve_plain(int B, int64_t L);
   int64_t plane_floats(int B, int T, int pad) const;
   int64_t cond_floats(int B) const;
   int amax_groups() const;
@@ -117,6 +131,8 @@ class Hifigan {
   size_t weights_bytes_ = 0;
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;
+  float* win_ = nullptr;  // windowed forward: gathered mel window [B][C][W] + window output [B][hop*W]
+  size_t win_bytes_ = 0;
 };
 
 }  // namespace tts

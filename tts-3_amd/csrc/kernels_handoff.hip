@@ -144,4 +144,23 @@ void launch_wav_int16(const float* wav, int B, int64_t n, const int64_t* len, un
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------------------
+// One time window of the replicate-padded mel (windowed HiFiGAN forward, hifigan.cpp)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) mel_window_kernel(const float* __restrict__ mel, int T, int pad, int64_t w0,
+                                                         int W, float* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= W) return;
+  const size_t row = (size_t)blockIdx.z * gridDim.y + blockIdx.y;  // b * C + c
+  int64_t src = w0 + t - pad;
+  src = src < 0 ? 0 : (src >= T ? T - 1 : src);
+  out[row * W + t] = mel[row * (size_t)T + src];
+}
+
+void launch_mel_window(const float* mel, int B, int C, int T, int pad, int64_t w0, int W, float* out, hipStream_t s) {
+  TTS_REQUIRE(B >= 1 && C >= 1 && C <= 65535 && B <= 65535 && T >= 1 && W >= 1, 1, "mel_window: bad shape");
+  hipLaunchKernelGGL(mel_window_kernel, dim3((W + 255) / 256, C, B), dim3(256), 0, s, mel, T, pad, w0, W, out);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts

@@ -300,7 +300,7 @@ class HifiganGenerator(nn.Module):
         x = c.to(device=dev, dtype=torch.float32).contiguous()
         B, C, T = x.shape
         out = torch.empty(B, self._cfg.out_channels, self.hop_length * (T + 2 * pad), device=dev)
-        cap = 512
+        cap = 4096  # windowed long utterances run ~80 launches per window
         recs = (N.TtsLaunchRecord * cap)()
         n = ctypes.c_int(0)
         N.call("tts_hifigan_forward_profiled", h, N.ptr(x), B, C, T, pad, None, N.ptr(out),
