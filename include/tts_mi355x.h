@@ -225,7 +225,8 @@ typedef struct TtsGlowEncoderCfg {
   int rel_attn_window_size; /* 0 = None (Glow-TTS default); 4 in the VITS-style encoders */
   int mean_only;            /* 1 (GlowTTSConfig default): x_logs = zeros */
   int use_prenet;           /* 1: ResidualConv1dLayerNormBlock(k5, 3 layers) before the transformer */
-  int c_in_channels;        /* 0 (speaker-conditioned duration predictor not implemented: must be 0) */
+  int c_in_channels;        /* 0 = unconditioned; > 0: speaker vector size, the duration predictor reads
+                               cat(x, g.expand(T)) (encoder.py:166-168; GlowTTS c_in_channels) */
   int math_mode;            /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
 } TtsGlowEncoderCfg;
 
@@ -241,7 +242,7 @@ typedef struct TtsGlowEncoderCfg {
  *       ffn_layers.l.conv_1.weight [ffn][H][k], bias [ffn], conv_2.weight [H][ffn][k], bias [H]
  *       norm_layers_2.l.gamma [H], beta [H]
  *   proj_m.weight [out][H][1], bias [out];  if !mean_only: proj_s.weight, bias
- *   duration_predictor.conv_1.weight [dp][H][3], bias, norm_1.gamma, beta,
+ *   duration_predictor.conv_1.weight [dp][H + c_in_channels][3], bias, norm_1.gamma, beta,
  *                      conv_2.weight [dp][dp][3], bias, norm_2.gamma, beta,
  *                      proj.weight [1][dp][1], proj.bias [1] */
 int tts_glow_encoder_num_weights(const TtsGlowEncoderCfg* cfg);
@@ -249,13 +250,17 @@ int64_t tts_glow_encoder_weight_numel(const TtsGlowEncoderCfg* cfg, int idx);
 int tts_glow_encoder_create(const TtsGlowEncoderCfg* cfg, const float* const* host_weights, int device,
                             void** handle);
 int tts_glow_encoder_destroy(void* handle);
-/* (x_m, x_logs, logw, x_mask) = Encoder.forward(tokens, lengths): tokens [B][T] int64 (ids in
- * [0, num_chars); padded positions may hold any id), lengths [B] int64; outputs x_m, x_logs
- * [B][out][T], logw [B][1][T], x_mask [B][1][T].  x_logs may be NULL when mean_only.  T <= 3072. */
-int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
-                             float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask, void* hip_stream);
-int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
-                                      int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+/* (x_m, x_logs, logw, x_mask) = Encoder.forward(tokens, lengths, g): tokens [B][T] int64 (ids in
+ * [0, num_chars); padded positions may hold any id), lengths [B] int64, d_g the speaker vector
+ * [B][c_in_channels] (the reference's g [B][c_in][1]; NULL when c_in_channels == 0); outputs x_m,
+ * x_logs [B][out][T], logw [B][1][T], x_mask [B][1][T].  x_logs may be NULL when mean_only.
+ * T <= 3072. */
+int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, const float* d_g,
+                             int B, int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+                             void* hip_stream);
+int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                      const float* d_g, int B, int T, float* d_x_m, float* d_x_logs, float* d_logw,
+                                      float* d_x_mask,
                                       void* hip_stream, TtsLaunchRecord* records, int max_records,
                                       int* n_records);
 

@@ -79,8 +79,9 @@ def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None):
 
 def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: torch.Tensor,
                     hidden_channels: int = 192, encoder_params: Optional[dict] = None, mean_only: bool = True,
-                    use_prenet: bool = True, dtype=torch.float64, **_unused):
-    """Encoder.forward(x, x_lengths) -> (x_m, x_logs, logw, x_mask) (encoder.py:143-179)."""
+                    use_prenet: bool = True, dtype=torch.float64, g: Optional[torch.Tensor] = None, **_unused):
+    """Encoder.forward(x, x_lengths, g) -> (x_m, x_logs, logw, x_mask) (encoder.py:143-179); g [B, c_in, 1]
+    is expanded over time and concatenated to the duration predictor's input (:166-168)."""
     ep = encoder_params or {"kernel_size": 3, "num_layers": 6, "num_heads": 2, "hidden_channels_ffn": 768}
     w = {k: v.to(dtype) for k, v in sd.items()}
     H = hidden_channels
@@ -118,7 +119,8 @@ def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: 
     else:
         x_logs = F.conv1d(x, w["proj_s.weight"], w["proj_s.bias"]) * x_mask
     d = "duration_predictor"  # duration_predictor.py:63-73
-    h = F.conv1d(x * x_mask, w[f"{d}.conv_1.weight"], w[f"{d}.conv_1.bias"], padding=1)
+    x_dp = x if g is None else torch.cat([x, g.to(dtype).expand(-1, -1, x.size(-1))], 1)
+    h = F.conv1d(x_dp * x_mask, w[f"{d}.conv_1.weight"], w[f"{d}.conv_1.bias"], padding=1)
     h = layer_norm(torch.relu(h), w[f"{d}.norm_1.gamma"], w[f"{d}.norm_1.beta"])
     h = F.conv1d(h * x_mask, w[f"{d}.conv_2.weight"], w[f"{d}.conv_2.bias"], padding=1)
     h = layer_norm(torch.relu(h), w[f"{d}.norm_2.gamma"], w[f"{d}.norm_2.beta"])

@@ -73,7 +73,8 @@ def _ref_encoder(Encoder, cfg, seed):
     torch.manual_seed(0)
     ref = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
                   "rel_pos_transformer", dict(cfg["encoder_params"]), dropout_p_dp=0.1,
-                  mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"], c_in_channels=0)
+                  mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"],
+                  c_in_channels=cfg.get("c_in_channels", 0))
     sd = synthetic.glow_encoder_state_dict(**cfg, seed=seed)
     ref.load_state_dict(sd)
     ref.eval()
@@ -103,23 +104,32 @@ def glow_tts_case(Encoder, Decoder, generate_path, sequence_mask, name, ecfg, dc
                   tok_seed, noise_scale, length_scale):
     """Tokens -> Encoder -> GlowTTS.inference glue (glow_tts.py:349-363) -> Decoder reverse, fp32 and
     fp64.  GlowTTS itself imports coqpit/trainer (absent), so the glue's 12 lines are restated here
-    around the reference's own generate_path / sequence_mask; the noise is drawn here and stored."""
+    around the reference's own generate_path / sequence_mask; the noise is drawn here and stored.
+    With ``c_in_channels`` in the configs (multi-speaker), d-vectors are drawn and stored and
+    g = F.normalize(d).unsqueeze(-1) as _speaker_embedding does (glow_tts.py:189-190)."""
     enc = _ref_encoder(Encoder, ecfg, eseed)
     torch.manual_seed(0)
     dec = Decoder(dcfg["in_channels"], dcfg["hidden_channels"], dcfg["kernel_size"], dcfg["dilation_rate"],
                   dcfg["num_flow_blocks"], dcfg["num_coupling_layers"], dropout_p=0.05,
                   num_splits=dcfg["num_splits"], num_squeeze=dcfg["num_squeeze"], sigmoid_scale=False,
-                  c_in_channels=0)
+                  c_in_channels=dcfg.get("c_in_channels", 0))
     dec.load_state_dict(synthetic.glow_decoder_state_dict(**dcfg, seed=dseed))
     dec.eval()
     dec.store_inverse()
     tok = synthetic.tokens(B, T, ecfg["num_chars"], seed=tok_seed)
     lens = torch.tensor(lengths)
     arrays = dict(tokens=tok.numpy(), lengths=lens.numpy())
+    c_in = ecfg.get("c_in_channels", 0)
+    assert c_in == dcfg.get("c_in_channels", 0)
+    d_vectors = None
+    if c_in:
+        d_vectors = torch.randn(B, c_in, generator=torch.Generator().manual_seed(tok_seed + 200))
+        arrays["d_vectors"] = d_vectors.numpy()
 
     def infer(e, d, dtype, noise):
+        g = None if d_vectors is None else torch.nn.functional.normalize(d_vectors.to(dtype)).unsqueeze(-1)
         with torch.no_grad():
-            o_mean, o_log_scale, o_dur_log, x_mask = e(tok, lens)
+            o_mean, o_log_scale, o_dur_log, x_mask = e(tok, lens, g=g)
             w = (torch.exp(o_dur_log) - 1) * x_mask * length_scale
             w_ceil = torch.clamp_min(torch.ceil(w), 1)
             y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
@@ -132,7 +142,7 @@ def glow_tts_case(Encoder, Decoder, generate_path, sequence_mask, name, ecfg, dc
             if noise is None:
                 noise = torch.randn(y_mean.shape, generator=torch.Generator().manual_seed(tok_seed + 100))
             z = (y_mean + torch.exp(y_log_scale) * noise.to(dtype) * noise_scale) * y_mask
-            y, _ = d(z, y_mask, reverse=True)
+            y, _ = d(z, y_mask, g=g, reverse=True)
         out = dict(x_m=o_mean, logw=o_dur_log, x_mask=x_mask, w=w, w_ceil=w_ceil, y_lengths=y_lengths,
                    y_mask=y_mask, attn=attn.squeeze(1), y_mean=y_mean, o_attn_dur=o_attn_dur, z=z, mel=y)
         return out, noise
@@ -286,6 +296,8 @@ def main():
         return main_handoff()
     if len(sys.argv) > 1 and sys.argv[1] == "xtts":
         return main_xtts()
+    if len(sys.argv) > 1 and sys.argv[1] == "glow_tts_spk":
+        return main_glow_tts_spk()
     if len(sys.argv) > 1 and sys.argv[1] == "glow_cond":
         return main_glow_cond()
     HifiganGenerator, Decoder = import_reference()
@@ -354,6 +366,20 @@ def main_glow_tts():
                                 "hidden_channels_ffn": 192, "rel_attn_window_size": 4},
                 mean_only=False, use_prenet=False)
     glow_encoder_case(Encoder, "glow_encoder_rel_b2_t19", rcfg, seed=97, B=2, T=19, lengths=[19, 11], tok_seed=43)
+
+
+def main_glow_tts_spk():
+    """G12: multi-speaker Glow-TTS (use_d_vector_file, d_vector_dim 72): g conditions the duration
+    predictor's input (encoder.py:166-168) and every flow's WN cond_layer (glow.py:143-150)."""
+    Encoder, Decoder, generate_path, sequence_mask = import_reference_glow_tts()
+    from tts_amd.config import GLOW_TTS_ENCODER
+
+    dcfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+                num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    ecfg_s = dict(GLOW_TTS_ENCODER, num_chars=64, c_in_channels=72)
+    dcfg_s = dict(dcfg, c_in_channels=72)
+    glow_tts_case(Encoder, Decoder, generate_path, sequence_mask, "glow_tts_spk_b2_t19", ecfg_s, dcfg_s, eseed=2468,
+                  dseed=1357, B=2, T=19, lengths=[19, 12], tok_seed=47, noise_scale=0.33, length_scale=1.0)
 
 
 def main_xtts():

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 110
+    assert N.lib().tts_abi_version() == 111
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -262,10 +262,50 @@ def test_glow_encoder_c_validation_codes():
                             hidden_channels_ffn=768, num_heads=5, num_layers=6, kernel_size=3)
     assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID  # transformer.py:75
     assert b"num_heads" in N.lib().tts_last_error()
-    c.num_heads, c.c_in_channels = 2, 16
-    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c.num_heads = 2
+    n0 = N.lib().tts_glow_encoder_num_weights(ctypes.byref(c))
+    assert n0 > 0
+    c.c_in_channels = 16  # speaker-conditioned duration predictor: same tensors, conv_1 [dp][H + 16][3]
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == n0
+    c.c_in_channels = -1
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
     c.c_in_channels, c.math_mode = 0, N.MATH_MODES["f16x3"]
     assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+
+
+def test_glow_tts_multispeaker_surface():
+    """init_multispeaker (glow_tts.py:107-135): use_speaker_embedding -> emb_g [num_speakers, H_enc] and
+    c_in = H_enc; use_d_vector_file -> c_in = d_vector_dim (512 by default).  The reference key set loads
+    strictly, the duration predictor's conv_1 takes H + c_in inputs, and _set_speaker_input's
+    errors (:170-174) are raised before any device work."""
+    from tts_amd.tts import GlowTTS
+
+    m = GlowTTS(dict(num_chars=64, use_speaker_embedding=True, num_speakers=7))
+    assert m.c_in_channels == 192 and m.encoder.c_in_channels == 192 and m.decoder.c_in_channels == 192
+    assert list(m.state_dict())[0] == "emb_g.weight" and m.emb_g.weight.shape == (7, 192)
+    ecfg = _glow_tts_cfg(c_in_channels=192)
+    esd = synthetic.glow_encoder_state_dict(**ecfg, seed=3)
+    assert esd["duration_predictor.conv_1.weight"].shape == (256, 384, 3)
+    m.encoder.load_state_dict(esd)
+    ws = m.encoder._weight_list()
+    assert len(ws) == N.lib().tts_glow_encoder_num_weights(ctypes.byref(m.encoder._cfg))
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_encoder_weight_numel(ctypes.byref(m.encoder._cfg), i) == w.size
+    tok, lens = torch.zeros(2, 5, dtype=torch.int64), torch.tensor([5, 3])
+    with pytest.raises(ValueError, match="together"):
+        m.inference(tok, {"x_lengths": lens, "speaker_ids": torch.tensor([0, 1]), "d_vectors": torch.zeros(2, 192)})
+    with pytest.raises(ValueError, match="speaker_ids or d_vectors"):
+        m.inference(tok, {"x_lengths": lens})
+    d = GlowTTS(dict(num_chars=64, use_d_vector_file=True))
+    assert d.c_in_channels == 512 and not hasattr(d, "emb_g")
+    assert GlowTTS(dict(num_chars=64, use_d_vector_file=True, d_vector_dim=256)).decoder.c_in_channels == 256
+    with pytest.raises(ValueError, match="without enabling speaker embedding"):
+        d.inference(tok, {"x_lengths": lens, "speaker_ids": torch.tensor([0, 1])})
+    single = GlowTTS(dict(num_chars=64))
+    with pytest.raises(ValueError, match="single-speaker"):
+        single.inference(tok, {"x_lengths": lens, "d_vectors": torch.zeros(2, 64)})
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        m.encoder(tok, lens, g=torch.zeros(2, 192, 1))
 
 
 @pytest.mark.parametrize("over,code", [

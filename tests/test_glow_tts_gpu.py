@@ -28,18 +28,30 @@ MEL_REL_RMS = 5e-6
 def build_encoder(cfg, seed, device, math_mode="fp32x6"):
     e = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
                 "rel_pos_transformer", cfg["encoder_params"], mean_only=cfg["mean_only"],
-                use_prenet=cfg["use_prenet"], math_mode=math_mode)
+                use_prenet=cfg["use_prenet"], c_in_channels=cfg.get("c_in_channels", 0), math_mode=math_mode)
     e.load_state_dict(synthetic.glow_encoder_state_dict(**cfg, seed=seed))
     e.eval()
     return e.to(device)
 
 
-def build_glow_tts(meta, device, decoder_math_mode="fp32"):
+def speaker_g(arr):
+    """the fixture's d-vectors -> g = F.normalize(d).unsqueeze(-1) (glow_tts.py:189-190), or None"""
+    if "d_vectors" not in arr:
+        return None
+    return torch.nn.functional.normalize(torch.from_numpy(arr["d_vectors"])).unsqueeze(-1)
+
+
+def build_glow_tts(meta, device, decoder_math_mode="fp32", **speaker):
     ecfg, dcfg = meta["encoder"], meta["decoder"]
+    c_in = ecfg.get("c_in_channels", 0)
+    if c_in and not speaker:
+        speaker = dict(use_d_vector_file=True, d_vector_dim=c_in)
     m = GlowTTS(dict(num_chars=ecfg["num_chars"], inference_noise_scale=meta["noise_scale"],
-                     length_scale=meta["length_scale"]), decoder_math_mode=decoder_math_mode)
+                     length_scale=meta["length_scale"], **speaker), decoder_math_mode=decoder_math_mode)
     sd = {f"encoder.{k}": v for k, v in synthetic.glow_encoder_state_dict(**ecfg, seed=meta["eseed"]).items()}
     sd.update({f"decoder.{k}": v for k, v in synthetic.glow_decoder_state_dict(**dcfg, seed=meta["dseed"]).items()})
+    if hasattr(m, "emb_g"):
+        sd["emb_g.weight"] = meta["emb_g"]
     m.load_state_dict(sd)
     m.eval()
     m.store_inverse()
@@ -54,7 +66,8 @@ def test_encoder_vs_reference(cuda_device, name, meta, arr, mode):
     e = build_encoder(meta["config"], meta["seed"], cuda_device, mode)
     tok = torch.from_numpy(arr["tokens"]).to(cuda_device)
     lens = torch.from_numpy(arr["lengths"]).to(cuda_device)
-    x_m, x_logs, logw, x_mask = e(tok, lens)
+    g = speaker_g(arr)
+    x_m, x_logs, logw, x_mask = e(tok, lens, None if g is None else g.to(cuda_device))
     assert torch.equal(x_mask.cpu(), torch.from_numpy(arr["x_mask_ref_fp64"]).float())
     assert_close_fp32(x_m.cpu(), arr["x_m_ref_fp64"], f"{name} x_m", ENC_MAX_ABS, ENC_REL_RMS)
     assert_close_fp32(logw.cpu(), arr["logw_ref_fp64"], f"{name} logw", ENC_MAX_ABS, ENC_REL_RMS)
@@ -122,7 +135,10 @@ def test_glow_tts_inference_end_to_end(cuda_device, name, meta, arr):
     """tokens -> GlowTTS.inference -> mel, with the fixture's sampling noise."""
     m = build_glow_tts(meta, cuda_device)
     tok = torch.from_numpy(arr["tokens"])
-    out = m.inference(tok, {"x_lengths": torch.from_numpy(arr["lengths"]), "noise": torch.from_numpy(arr["noise"])})
+    aux = {"x_lengths": torch.from_numpy(arr["lengths"]), "noise": torch.from_numpy(arr["noise"])}
+    if "d_vectors" in arr:
+        aux["d_vectors"] = torch.from_numpy(arr["d_vectors"])
+    out = m.inference(tok, aux)
     # durations are ceil()-quantised: the fixture keeps every w >= 1.8e-2 away from an integer
     # (meta ceil_margin), so the fp32 encoder must reproduce the reference alignment exactly
     assert torch.equal(out["alignments"].cpu(), torch.from_numpy(arr["attn_ref_fp64"]).permute(0, 2, 1).float())
@@ -166,3 +182,40 @@ def test_glow_tts_batch_invariance_and_determinism(cuda_device):
     T5 = mel.shape[2]
     assert_close_fp32(a["model_outputs"][5, :T5].transpose(0, 1).cpu(), mel[0], "ragged row 5", MEL_MAX_ABS,
                       MEL_REL_RMS)
+
+
+def test_multispeaker_speaker_ids_vs_oracle(cuda_device):
+    """use_speaker_embedding (glow_tts.py:129-133): g = F.normalize(emb_g(speaker_ids)) of width
+    hidden_channels_enc conditions the duration predictor and the 12 flows; each utterance against
+    the oracle chain (fp64) with its own speaker vector, and a speaker swap changes durations and mel."""
+    H = GLOW_TTS_ENCODER["hidden_channels"]
+    ecfg = dict(GLOW_TTS_ENCODER, num_chars=64, c_in_channels=H)
+    dcfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+                num_coupling_layers=4, num_splits=4, num_squeeze=2, c_in_channels=H)
+    emb = torch.rand(5, H, generator=torch.Generator().manual_seed(9)) * 0.2 - 0.1
+    meta = dict(encoder=ecfg, decoder=dcfg, eseed=21, dseed=22, noise_scale=0.0, length_scale=1.0, emb_g=emb)
+    m = build_glow_tts(meta, cuda_device, use_speaker_embedding=True, num_speakers=5)
+    assert m.c_in_channels == H and m.encoder.c_in_channels == H and m.decoder.c_in_channels == H
+    tok = synthetic.tokens(3, 31, 64, seed=12)
+    lens = torch.tensor([31, 25, 9])
+    sid = torch.tensor([4, 0, 2])
+    out = m.inference(tok, {"x_lengths": lens, "speaker_ids": sid})
+    esd = synthetic.glow_encoder_state_dict(**ecfg, seed=21)
+    dsd = synthetic.glow_decoder_state_dict(**dcfg, seed=22)
+    g = torch.nn.functional.normalize(emb[sid].double()).unsqueeze(-1)
+    for b in range(3):
+        xm_, _, logw, xmask = glow_tts_ref.encoder_forward(esd, tok[b:b + 1], lens[b:b + 1], g=g[b:b + 1])
+        w_ceil, ylen = glow_tts_ref.durations(logw, xmask)
+        z, ymask, *_ = glow_tts_ref.expand(w_ceil, xmask, ylen, xm_, torch.zeros_like(xm_))
+        mel = glow_ref.glow_decoder_reverse(dsd, z, ymask, g=g[b:b + 1], **dcfg)
+        Tb = mel.shape[2]
+        assert_close_fp32(out["durations_log"][b, :lens[b]].transpose(0, 1).cpu(), logw[0, :, :lens[b]],
+                          f"logw spk {int(sid[b])}", ENC_MAX_ABS, ENC_REL_RMS)
+        assert_close_fp32(out["model_outputs"][b, :Tb].transpose(0, 1).cpu(), mel[0], f"mel spk {int(sid[b])}",
+                          MEL_MAX_ABS, MEL_REL_RMS)
+    other = m.inference(tok, {"x_lengths": lens, "speaker_ids": torch.tensor([1, 3, 0])})
+    assert not torch.equal(other["durations_log"], out["durations_log"])
+    with pytest.raises(ValueError):
+        m.inference(tok, {"x_lengths": lens})
+    with pytest.raises(ValueError):
+        m.inference(tok, {"x_lengths": lens, "speaker_ids": sid, "d_vectors": torch.zeros(3, H)})

@@ -134,13 +134,21 @@ def test_glow_encoder_oracle_matches_reference(name, meta, arr):
     cfg = meta["config"]
     sd = synthetic.glow_encoder_state_dict(**cfg, seed=meta["seed"])
     tok, lens = torch.from_numpy(arr["tokens"]), torch.from_numpy(arr["lengths"])
-    out = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float64, **_enc_args(cfg))
+    g = _speaker_g(arr)
+    out = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float64, g=g, **_enc_args(cfg))
     for n, o in zip(["x_m", "x_logs", "logw", "x_mask"], out):
         if f"{n}_ref_fp64" in arr:
             assert max_abs(o.numpy(), arr[f"{n}_ref_fp64"]) < 1e-10, n
-    out32 = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float32, **_enc_args(cfg))
+    out32 = glow_tts_ref.encoder_forward(sd, tok, lens, dtype=torch.float32, g=g, **_enc_args(cfg))
     assert max_abs(out32[0].numpy(), arr["x_m_ref_fp32"]) < 1e-5
     assert max_abs(out32[2].numpy(), arr["logw_ref_fp32"]) < 1e-5
+
+
+def _speaker_g(arr):
+    """multi-speaker fixtures store d-vectors; g = F.normalize(d).unsqueeze(-1) (glow_tts.py:189-190)"""
+    if "d_vectors" not in arr:
+        return None
+    return torch.nn.functional.normalize(torch.from_numpy(arr["d_vectors"]).double()).unsqueeze(-1)
 
 
 @pytest.mark.parametrize("name,meta,arr", GTTS, ids=[g[0] for g in GTTS])
@@ -162,7 +170,7 @@ def test_glow_tts_glue_oracle_matches_reference(name, meta, arr):
     # then the decoder oracle closes the chain to the reference's mel
     dcfg = meta["decoder"]
     dsd = synthetic.glow_decoder_state_dict(**dcfg, seed=meta["dseed"])
-    mel = glow_ref.glow_decoder_reverse(dsd, z, y_mask, dtype=torch.float64, **dcfg)
+    mel = glow_ref.glow_decoder_reverse(dsd, z, y_mask, dtype=torch.float64, g=_speaker_g(arr), **dcfg)
     assert max_abs(mel.numpy(), arr["mel_ref_fp64"]) < 1e-10
     # ceil() margin: no duration of the fixture sits within 1e-3 of an integer, so an fp32
     # implementation that matches the encoder to ~1e-6 must reproduce w_ceil exactly

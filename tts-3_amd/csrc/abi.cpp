@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 110; }
+int tts_abi_version(void) { return 111; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -188,17 +188,19 @@ int tts_glow_encoder_destroy(void* handle) {
   return guarded([&] { delete static_cast<tts::GlowEncoder*>(handle); });
 }
 
-int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
-                             float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask, void* hip_stream) {
+int tts_glow_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, const float* d_g,
+                             int B, int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+                             void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
-    static_cast<tts::GlowEncoder*>(handle)->forward(d_tokens, d_lengths, B, T, d_x_m, d_x_logs, d_logw, d_x_mask,
-                                                    static_cast<hipStream_t>(hip_stream));
+    static_cast<tts::GlowEncoder*>(handle)->forward(d_tokens, d_lengths, d_g, B, T, d_x_m, d_x_logs, d_logw,
+                                                    d_x_mask, static_cast<hipStream_t>(hip_stream));
   });
 }
 
-int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
-                                      int T, float* d_x_m, float* d_x_logs, float* d_logw, float* d_x_mask,
+int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                      const float* d_g, int B, int T, float* d_x_m, float* d_x_logs, float* d_logw,
+                                      float* d_x_mask,
                                       void* hip_stream, TtsLaunchRecord* records, int max_records,
                                       int* n_records) {
   return guarded([&] {
@@ -208,7 +210,7 @@ int tts_glow_encoder_forward_profiled(void* handle, const int64_t* d_tokens, con
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->forward(d_tokens, d_lengths, B, T, d_x_m, d_x_logs, d_logw, d_x_mask, s, &prof);
+      h->forward(d_tokens, d_lengths, d_g, B, T, d_x_m, d_x_logs, d_logw, d_x_mask, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);

@@ -44,7 +44,8 @@ std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
   }
   n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels);  // proj_m
   if (!c.mean_only) { n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels); }  // proj_s
-  n.push_back(D * H * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_1, norm_1
+  // dp conv_1 reads cat(x, g) when speaker-conditioned (encoder.py:166-168: H + c_in channels)
+  n.push_back(D * (H + c.c_in_channels) * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_1, norm_1
   n.push_back(D * D * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_2, norm_2
   n.push_back(D); n.push_back(1);                                           // dp proj
   return n;
@@ -61,7 +62,7 @@ void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
                   c.kernel_size == 11,
               3, "FFN kernel_size must be 1, 3, 5, 7 or 11");
   TTS_REQUIRE(c.rel_attn_window_size >= 0, 1, "rel_attn_window_size must be >= 0 (0 = None)");
-  TTS_REQUIRE(c.c_in_channels == 0, 3, "speaker-conditioned duration predictor (c_in_channels > 0) not implemented");
+  TTS_REQUIRE(c.c_in_channels >= 0, 1, "c_in_channels must be >= 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
   TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3,
               "Glow encoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
@@ -154,7 +155,7 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
     put_conv(proj_s_, {{hw[wi], hw[wi + 1]}}, cfg_.out_channels, H, 1);
     wi += 2;
   }
-  put_conv(dp1_, {{hw[wi], hw[wi + 1]}}, D, H, 3);
+  put_conv(dp1_, {{hw[wi], hw[wi + 1]}}, D, H + cfg_.c_in_channels, 3);
   put_norm(dpn1_, hw[wi + 2], hw[wi + 3], D);
   put_conv(dp2_, {{hw[wi + 4], hw[wi + 5]}}, D, D, 3);
   put_norm(dpn2_, hw[wi + 6], hw[wi + 7], D);
@@ -177,19 +178,21 @@ void GlowEncoder::reserve(int B, int T) {
   const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, D = cfg_.hidden_channels_dp;
   const size_t plane = (size_t)B * T;
   const size_t big = std::max({(size_t)3 * H, (size_t)F, (size_t)D});
-  const size_t need = plane * (3 * (size_t)H + big + std::max((size_t)H, (size_t)D)) * sizeof(float) + 4096;
+  const size_t dpin = cfg_.c_in_channels > 0 ? plane * (H + cfg_.c_in_channels) + 64 : 0;  // cat(x, g) * mask
+  const size_t need = (plane * (3 * (size_t)H + big + std::max((size_t)H, (size_t)D)) + dpin) * sizeof(float) + 4096;
   if (need <= ws_bytes_) return;
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
   ws_bytes_ = need;
 }
 
-void GlowEncoder::forward(const int64_t* tok, const int64_t* len, int B, int T, float* x_m, float* x_logs,
-                          float* logw, float* x_mask, hipStream_t s, Profiler* prof) {
+void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m,
+                          float* x_logs, float* logw, float* x_mask, hipStream_t s, Profiler* prof) {
   TTS_REQUIRE(tok && len && x_m && logw && x_mask, 1, "NULL input/output pointer");
+  TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1 && T >= 1, 1, "batch and token count must be >= 1");
   TTS_REQUIRE(T <= ATTN_MAX_T, 3, "more than " + std::to_string(ATTN_MAX_T) + " tokens per utterance");
-  DeviceGuard g(device_);
+  DeviceGuard dg(device_);
   reserve(B, T);
   const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, D = cfg_.hidden_channels_dp;
   const int mode = cfg_.math_mode;
@@ -202,7 +205,8 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, int B, int T, 
   float* A = p; p += al(plane * H);    // attention output
   const size_t big = std::max({(size_t)3 * H, (size_t)F, (size_t)D});
   float* Wd = p; p += al(plane * big);  // qkv / FFN hidden / dp hidden
-  float* Nb = p;                         // LayerNorm output of prenet / dp (max(H, D) rows)
+  float* Nb = p; p += al(plane * std::max((size_t)H, (size_t)D));  // LayerNorm output of prenet / dp
+  float* Xdp = cfg_.c_in_channels > 0 ? p : nullptr;                // dp input cat(x, g) * mask
   const float* mask = x_mask;
   constexpr float kEps = 1e-4f;  // normalization.py:6
 
@@ -259,8 +263,17 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, int B, int T, 
   } else if (x_logs) {
     TTS_HIP_CHECK(hipMemsetAsync(x_logs, 0, plane * cfg_.out_channels * sizeof(float), s));
   }
-  // duration predictor (duration_predictor.py:63-73) on x (detached: same values)
-  conv("enc_dp_conv", dp1_, x, Wd, nullptr, mask, 0.f, false);
+  // duration predictor (duration_predictor.py:63-73) on x (detached: same values), or on
+  // cat(x, g.expand(T)) for a speaker-conditioned model (encoder.py:166-168; the predictor masks
+  // its whole input, :66, and x is already masked)
+  const float* xdp = x;
+  if (Xdp) {
+    const int Cc = cfg_.c_in_channels;
+    run(prof, s, "enc_dp_input", 0.0, 4.0 * P * (2 * H + Cc + 1),
+        [&] { launch_dp_input(x, g, mask, Xdp, B, H, Cc, T, s); });
+    xdp = Xdp;
+  }
+  conv("enc_dp_conv", dp1_, xdp, Wd, nullptr, mask, 0.f, false);
   norm("enc_layernorm", dpn1_, Wd, nullptr, Nb, D, false);
   conv("enc_dp_conv", dp2_, Nb, Wd, nullptr, mask, 0.f, false);
   norm("enc_layernorm", dpn2_, Wd, nullptr, Nb, D, false);

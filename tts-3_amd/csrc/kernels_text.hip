@@ -396,4 +396,28 @@ void launch_expand(const ExpandArgs& a, int B, hipStream_t s) {
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------------------
+// Speaker-conditioned duration predictor input (encoder.py:166-168)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) dp_input_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                       const float* __restrict__ mask, float* __restrict__ xdp, int H,
+                                                       int Cg, int T) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  const int b = blockIdx.z;
+  if (t >= T) return;
+  const int C = H + Cg;
+  const float m = mask[(size_t)b * T + t];
+  // x_dp * x_mask with x_dp = cat(x, g.expand(T)); m is 0 or 1, so the product is exact
+  const float v = c < H ? x[((size_t)b * H + c) * T + t] : g[(size_t)b * Cg + (c - H)];
+  xdp[((size_t)b * C + c) * T + t] = v * m;
+}
+
+void launch_dp_input(const float* x, const float* g, const float* mask, float* xdp, int B, int H, int Cg, int T,
+                     hipStream_t s) {
+  TTS_REQUIRE(B >= 1 && B <= 65535 && H + Cg <= 65535 && T >= 1, 1, "dp_input: bad shape");
+  hipLaunchKernelGGL(dp_input_kernel, dim3((T + 255) / 256, H + Cg, B), dim3(256), 0, s, x, g, mask, xdp, H, Cg, T);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts

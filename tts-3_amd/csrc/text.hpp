@@ -23,6 +23,10 @@ void launch_layernorm(const float* a, const float* r, const float* gamma, const 
 // out[B][H][T] = multi-head attention of qkv [B][3H][T] (W = 0: no relative embeddings)
 void launch_attention(const float* qkv, const float* mask, const float* ek, const float* ev, float* out, int B,
                       int H, int heads, int T, int W, hipStream_t s);
+// xdp[b][c][t] = (c < H ? x[b][c][t] : g[b][c - H]) * mask[b][t]: the speaker-conditioned duration
+// predictor's input cat(x, g.expand(T)) (encoder.py:166-168, masked at duration_predictor.py:66)
+void launch_dp_input(const float* x, const float* g, const float* mask, float* xdp, int B, int H, int Cg, int T,
+                     hipStream_t s);
 void launch_durations(const float* logw, const float* xm, float* w_ceil, int64_t* y_len, float* dur, int B, int T,
                       float length_scale, hipStream_t s);
 
@@ -52,8 +56,9 @@ class GlowEncoder {
   ~GlowEncoder();
   GlowEncoder(const GlowEncoder&) = delete;
   GlowEncoder& operator=(const GlowEncoder&) = delete;
-  void forward(const int64_t* tok, const int64_t* len, int B, int T, float* x_m, float* x_logs, float* logw,
-               float* x_mask, hipStream_t s, Profiler* prof = nullptr);
+  // g: [B][c_in_channels] speaker vector (the reference's g [B][c_in][1]), NULL when c_in_channels == 0
+  void forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m, float* x_logs,
+               float* logw, float* x_mask, hipStream_t s, Profiler* prof = nullptr);
   int device() const { return device_; }
 
  private:

@@ -178,11 +178,11 @@ SIGNATURES = {
     ),
     "tts_glow_encoder_destroy": (c_int, [c_void_p]),
     "tts_glow_encoder_forward": (
-        c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     ),
     "tts_glow_encoder_forward_profiled": (
         c_int,
-        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_glow_durations": (

@@ -234,6 +234,7 @@ def glow_encoder_state_dict(
     encoder_params: Dict = None,
     mean_only: bool = GLOW_TTS_ENCODER["mean_only"],
     use_prenet: bool = GLOW_TTS_ENCODER["use_prenet"],
+    c_in_channels: int = 0,
     seed: int = 8642,
     log_duration: float = 1.6,
     **_unused,
@@ -294,7 +295,7 @@ def glow_encoder_state_dict(
     conv("proj_m", out_channels, H, 1)
     if not mean_only:
         conv("proj_s", out_channels, H, 1, 0.3)
-    conv("duration_predictor.conv_1", hidden_channels_dp, H, 3, 1.4)
+    conv("duration_predictor.conv_1", hidden_channels_dp, H + c_in_channels, 3, 1.4)  # [x; g] (encoder.py:140)
     norm("duration_predictor.norm_1", hidden_channels_dp)
     conv("duration_predictor.conv_2", hidden_channels_dp, hidden_channels_dp, 3, 1.4)
     norm("duration_predictor.norm_2", hidden_channels_dp)

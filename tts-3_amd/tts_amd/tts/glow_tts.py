@@ -12,8 +12,10 @@
   the ``model`` state dict with ``torch.load(weights_only=True)``.
 
 The nn modules below only hold parameters; the handle is rebuilt when any parameter changes.
-The other encoder types (gated_conv, residual_conv_bn, time_depth_separable), speaker
-conditioning and training (``forward``, MAS) are outside the MI355X path and raise.
+Multi-speaker models (``use_speaker_embedding`` / ``use_d_vector_file``, glow_tts.py:107-191)
+condition the duration predictor and the decoder flows on ``g``.  The other encoder types
+(gated_conv, residual_conv_bn, time_depth_separable) and training (``forward``, MAS) are
+outside the MI355X path and raise.
 """
 from __future__ import annotations
 
@@ -25,6 +27,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 from torch import nn
+from torch.nn import functional as F
 
 from .. import _native as N
 from ..config import GLOW_TTS_DECODER, GLOW_TTS_ENCODER, GLOW_TTS_INFERENCE
@@ -136,8 +139,6 @@ class Encoder(nn.Module):
         if encoder_type.lower() != "rel_pos_transformer":
             raise NotImplementedError(f"encoder_type '{encoder_type}' is not implemented on the MI355X path "
                                       "(only rel_pos_transformer, the Glow-TTS default)")
-        if c_in_channels:
-            raise NotImplementedError("speaker-conditioned duration predictor (c_in_channels > 0) not implemented")
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
         self.num_chars = num_chars
@@ -262,42 +263,57 @@ class Encoder(nn.Module):
         self._release()
         return super()._apply(fn, *args, **kwargs)
 
-    def _io(self, x, x_lengths):
+    def _speaker(self, g: Optional[torch.Tensor], B: int, dev: torch.device) -> Optional[torch.Tensor]:
+        """g [B, c_in, 1] (encoder.py:166-168 expands it over time) -> contiguous fp32 [B, c_in]."""
+        if not self.c_in_channels:
+            if g is not None:
+                raise ValueError("g given to an encoder built with c_in_channels=0")
+            return None
+        if g is None:
+            raise ValueError(f"this encoder is speaker-conditioned: g [B, {self.c_in_channels}, 1] is required")
+        if g.dim() == 3 and g.shape[-1] == 1:
+            g = g[..., 0]
+        if g.shape != (B, self.c_in_channels):
+            raise ValueError(f"g must be [{B}, {self.c_in_channels}, 1], got {tuple(g.shape)}")
+        return g.to(device=dev, dtype=torch.float32).contiguous()
+
+    def _io(self, x, x_lengths, g=None):
         dev = self._device()
         tok = x.to(device=dev, dtype=torch.int64).contiguous()
         lens = x_lengths.to(device=dev, dtype=torch.int64).contiguous()
         B, T = tok.shape
         if lens.shape != (B,):
             raise ValueError(f"x_lengths must be [B] = [{B}], got {tuple(lens.shape)}")
+        gv = self._speaker(g, B, dev)
         x_m = torch.empty(B, self.out_channels, T, device=dev)
         x_logs = torch.empty_like(x_m)
         logw = torch.empty(B, 1, T, device=dev)
         x_mask = torch.empty(B, 1, T, device=dev)
-        return dev, tok, lens, (x_m, x_logs, logw, x_mask)
+        return dev, tok, lens, gv, (x_m, x_logs, logw, x_mask)
 
     # ------------------------------------------------------------------ reference API
     def forward(self, x: torch.Tensor, x_lengths: torch.Tensor, g: Optional[torch.Tensor] = None):
-        """encoder.py:143-179: x [B, T] token ids, x_lengths [B] -> (x_m, x_logs, logw, x_mask)."""
-        if g is not None:
-            raise NotImplementedError("speaker conditioning (g) is not implemented on the MI355X path")
+        """encoder.py:143-179: x [B, T] token ids, x_lengths [B], g [B, c_in, 1] (speaker vector of a
+        c_in_channels > 0 encoder, concatenated to the duration predictor's input, :166-168)
+        -> (x_m, x_logs, logw, x_mask)."""
         with torch.no_grad():
             h = self._native_handle()
-            dev, tok, lens, outs = self._io(x, x_lengths)
+            dev, tok, lens, gv, outs = self._io(x, x_lengths, g)
             B, T = tok.shape
-            N.call("tts_glow_encoder_forward", h, N.ptr(tok), N.ptr(lens), B, T, *[N.ptr(o) for o in outs],
-                   N.stream_ptr(dev))
+            N.call("tts_glow_encoder_forward", h, N.ptr(tok), N.ptr(lens), N.ptr(gv), B, T,
+                   *[N.ptr(o) for o in outs], N.stream_ptr(dev))
         return outs
 
-    def profile(self, x: torch.Tensor, x_lengths: torch.Tensor):
+    def profile(self, x: torch.Tensor, x_lengths: torch.Tensor, g: Optional[torch.Tensor] = None):
         """One forward with a hipEvent pair around every launch: (outputs, [{name, flops, bytes, ms}])."""
         h = self._native_handle()
-        dev, tok, lens, outs = self._io(x, x_lengths)
+        dev, tok, lens, gv, outs = self._io(x, x_lengths, g)
         B, T = tok.shape
         cap = 1024
         recs = (N.TtsLaunchRecord * cap)()
         n = ctypes.c_int(0)
-        N.call("tts_glow_encoder_forward_profiled", h, N.ptr(tok), N.ptr(lens), B, T, *[N.ptr(o) for o in outs],
-               N.stream_ptr(dev), recs, cap, ctypes.byref(n))
+        N.call("tts_glow_encoder_forward_profiled", h, N.ptr(tok), N.ptr(lens), N.ptr(gv), B, T,
+               *[N.ptr(o) for o in outs], N.stream_ptr(dev), recs, cap, ctypes.byref(n))
         rows = [{"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
                 for i in range(min(n.value, cap))]
         return outs, rows
@@ -349,34 +365,73 @@ class GlowTTS(nn.Module):
         self.num_splits = get("num_splits", GLOW_TTS_DECODER["num_splits"])
         self.num_squeeze = get("num_squeeze", GLOW_TTS_DECODER["num_squeeze"])
         self.sigmoid_scale = get("sigmoid_scale", GLOW_TTS_DECODER["sigmoid_scale"])
-        self.c_in_channels = get("c_in_channels", 0)
         self.inference_noise_scale = get("inference_noise_scale", GLOW_TTS_INFERENCE["inference_noise_scale"])
         self.length_scale = get("length_scale", GLOW_TTS_INFERENCE["length_scale"])
-        if get("use_speaker_embedding", False) or get("use_d_vector_file", False) or self.c_in_channels:
-            raise NotImplementedError("multi-speaker Glow-TTS is not implemented on the MI355X path")
+        # init_multispeaker (glow_tts.py:107-135): emb_g is registered before the encoder, as there
+        self.num_speakers = get("num_speakers", 0)
+        self.use_speaker_embedding = get("use_speaker_embedding", False)
+        self.use_d_vector_file = get("use_d_vector_file", False)
+        self.embedded_speaker_dim = 0
+        if self.use_d_vector_file:
+            d = get("d_vector_dim", None)
+            self.embedded_speaker_dim = d if d is not None else 512
+        if self.use_speaker_embedding and not self.use_d_vector_file:
+            self.embedded_speaker_dim = self.hidden_channels_enc
+            self.emb_g = nn.Embedding(self.num_speakers, self.hidden_channels_enc)
+            nn.init.uniform_(self.emb_g.weight, -0.1, 0.1)
+        self.c_in_channels = self.embedded_speaker_dim
         self.encoder = Encoder(self.num_chars, out_channels=self.out_channels,
                                hidden_channels=self.hidden_channels_enc, hidden_channels_dp=self.hidden_channels_dp,
                                encoder_type=self.encoder_type, encoder_params=self.encoder_params,
                                mean_only=self.mean_only, use_prenet=self.use_encoder_prenet,
-                               dropout_p_dp=get("dropout_p_dp", 0.1), c_in_channels=0, math_mode=math_mode)
+                               dropout_p_dp=get("dropout_p_dp", 0.1), c_in_channels=self.c_in_channels,
+                               math_mode=math_mode)
         self.decoder = Decoder(self.out_channels, self.hidden_channels_dec, self.kernel_size_dec, self.dilation_rate,
                                self.num_flow_blocks_dec, self.num_block_layers,
                                dropout_p=get("dropout_p_dec", 0.05), num_splits=self.num_splits,
-                               num_squeeze=self.num_squeeze, sigmoid_scale=self.sigmoid_scale, c_in_channels=0,
+                               num_squeeze=self.num_squeeze, sigmoid_scale=self.sigmoid_scale,
+                               c_in_channels=self.c_in_channels,
                                math_mode=decoder_math_mode or math_mode)
 
     def _device(self) -> torch.device:
         return self.encoder._device()
 
+    def _set_speaker_input(self, aux_input: Optional[Dict]):  # glow_tts.py:162-177
+        d_vectors = None if aux_input is None else aux_input.get("d_vectors", None)
+        speaker_ids = None if aux_input is None else aux_input.get("speaker_ids", None)
+        if d_vectors is not None and speaker_ids is not None:
+            raise ValueError("[!] Cannot use d-vectors and speaker-ids together.")
+        if speaker_ids is not None and not hasattr(self, "emb_g"):
+            raise ValueError("[!] Cannot use speaker-ids without enabling speaker embedding.")
+        return speaker_ids if speaker_ids is not None else d_vectors
+
+    def _speaker_embedding(self, aux_input: Optional[Dict]) -> Optional[torch.Tensor]:  # glow_tts.py:179-191
+        """speaker ids -> F.normalize(emb_g(ids)) or d-vectors -> F.normalize(d): [B, c_in, 1].
+        A few hundred floats: the lookup and the normalisation stay in torch on the device."""
+        g = self._set_speaker_input(aux_input)
+        if g is None:
+            return None
+        if not self.c_in_channels:
+            raise ValueError("d_vectors given to a single-speaker model (use_d_vector_file=False)")
+        dev = self._device()
+        if hasattr(self, "emb_g"):
+            g = g.to(dev)
+            if not g.size():
+                g = g.unsqueeze(0)
+            return F.normalize(self.emb_g(g)).unsqueeze(-1)
+        return F.normalize(g.to(device=dev, dtype=torch.float32)).unsqueeze(-1)
+
     @torch.no_grad()
     def inference(self, x, aux_input={"x_lengths": None, "d_vectors": None, "speaker_ids": None}):  # noqa: B006
         """glow_tts.py:342-374.  ``aux_input["noise"]`` (optional, [B, out, T_y]) replaces
-        ``torch.randn_like(y_mean)`` so that a caller can pin the sampling noise."""
-        if aux_input.get("d_vectors") is not None or aux_input.get("speaker_ids") is not None:
-            raise NotImplementedError("multi-speaker Glow-TTS is not implemented on the MI355X path")
+        ``torch.randn_like(y_mean)`` so that a caller can pin the sampling noise.  ``speaker_ids``
+        or ``d_vectors`` condition a multi-speaker model (both encoder and decoder, :346-365)."""
         x_lengths = aux_input["x_lengths"]
+        g = self._speaker_embedding(aux_input)
+        if self.c_in_channels and g is None:
+            raise ValueError("multi-speaker Glow-TTS: pass aux_input speaker_ids or d_vectors")
         dev = self._device()
-        o_mean, o_log_scale, o_dur_log, x_mask = self.encoder(x, x_lengths)
+        o_mean, o_log_scale, o_dur_log, x_mask = self.encoder(x, x_lengths, g=g)
         B, C, T_x = o_mean.shape
         w_ceil = torch.empty(B, 1, T_x, device=dev)
         y_lengths = torch.empty(B, dtype=torch.int64, device=dev)
@@ -400,7 +455,7 @@ class GlowTTS(nn.Module):
         N.call("tts_glow_expand", N.ptr(w_ceil), N.ptr(x_mask), N.ptr(y_lengths), N.ptr(o_mean),
                N.ptr(None if self.mean_only else o_log_scale), N.ptr(noise), float(self.inference_noise_scale),
                B, C, T_x, T_y, N.ptr(z), N.ptr(y_mask), N.ptr(y_mean), N.ptr(y_log_scale), N.ptr(attn), stream)
-        y, logdet = self.decoder(z, y_mask, reverse=True)
+        y, logdet = self.decoder(z, y_mask, g=g, reverse=True)
         return {
             "model_outputs": y.transpose(1, 2),
             "logdet": logdet,
