@@ -146,14 +146,19 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, 
   // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
-  // XCD-aware tile order for multi-m-block launches (TTS_MI355X_XCD_REMAP=1 enables it; it measured
-  // neutral: the ConvTranspose weights re-read per XCD are served by the 256 MB Infinity Cache)
-  static const bool remap = [] {
+  // XCD-aware tile orders for multi-m-block launches (split_kernel.hpp), TTS_MI355X_XCD_REMAP:
+  //   1: an XCD's workgroups take one contiguous range with the m-block slowest (weights stay in
+  //      its L2; measured neutral: the weights re-read per XCD are served by the Infinity Cache)
+  //   2: the m-blocks of one column tile run together on one XCD (the input window is fetched
+  //      once per XCD instead of once per m-block)
+  static const int remap = [] {
     const char* e = std::getenv("TTS_MI355X_XCD_REMAP");
-    return e && e[0] == '1';  // measured neutral (MI355X A/B): off by default
+    return e ? std::atoi(e) : 0;
   }();
   Conv1dArgs ar = a;
-  ar.xcd_remap = remap && ceil_div(a.Cout, conv1d_split_tile(mode, tile).BM) > 1 ? 1 : 0;
+  const int gy = ceil_div(a.Cout, conv1d_split_tile(mode, tile).BM);
+  const int64_t nwg = (int64_t)ceil_div(a.Tout, conv1d_split_tile(mode, tile).BN) * gy * B;
+  ar.xcd_remap = gy > 1 && (remap == 1 || (remap == 2 && nwg % (8 * gy) == 0)) ? remap : 0;
   if (mode == MATH_FP32_F16X3) launch_split_h3(ar, B, K, tile, s);
   else if (mode == MATH_BF16) launch_split_b1(ar, B, K, tile, s);
   else launch_split_x6(ar, B, K, tile, s);

@@ -63,6 +63,7 @@ struct Wino8Cfg {
   static constexpr int UPW = (UNITS + 7) / 8;        // units per wave
   static constexpr int PITCH = 256;                  // epilogue transpose row (samples)
   static_assert(UPW <= 64 && UNITS <= 256 + 64 && 3 * NCH >= 3, "one transform round per wave; the DMA spreads over 3 steps");
+  static_assert(2 * (UNITS - 256) <= 4 * 64, "spread leftover jobs: one per lane of waves 4-7");
   static_assert(TW <= PITCH, "");
   static_assert(2 * TSZ >= 4 * 16 * PITCH * 4 && 2 * TSZ >= 8 * 8 * 4 * 64 * 4, "epilogue LDS (transformed buffers)");
 };
@@ -128,12 +129,23 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_DENSE
 #define WINO8_DENSE 1
 #endif
+#ifndef WINO8_SPREAD
+#define WINO8_SPREAD 1
+#endif
   // dense: waves 0-3 (which issue no HBM loads and so never wait on one) take units 0-255 with every
-  // lane, wave 4 the rest; else every wave takes UPW units (balanced, but only UPW of its 64 lanes
-  // active)
-  const int u = WINO8_DENSE ? (grp == 0 ? wave * 64 + lane : (wave == 4 ? 256 + lane : C::UNITS))
+  // lane, all four channel pieces each; else every wave takes UPW units (balanced, but only UPW of
+  // its 64 lanes active).  The units past 256 (the chunk halo: 4-40 of them): with WINO8_SPREAD
+  // each lane of waves 4-7 takes one (unit, piece pair) job, dealt round-robin over the four waves,
+  // so every SIMD runs the transform instructions of one full and one half pass; otherwise wave 4
+  // alone takes them whole and its SIMD runs two full passes per chunk while the others run one.
+  const int e = lane * 4 + (wave - 4);  // leftover job of a waves-4-7 lane
+  const int u = WINO8_DENSE ? (grp == 0 ? wave * 64 + lane
+                                        : (WINO8_SPREAD ? 256 + (e >> 1) : (wave == 4 ? 256 + lane : C::UNITS)))
                             : wave * C::UPW + lane;
   const bool uok = (WINO8_DENSE || lane < C::UPW) && u < C::UNITS;
+  // pieces a lane transforms: all four, or one pair (2 jp, 2 jp + 1) for a spread leftover job
+  constexpr bool SPREAD = WINO8_DENSE && WINO8_SPREAD;
+  const int jp = e & 1;
   const int urow = u >> 2, uq = u & 3;
   const int ujj = urow / D, urho = urow - (urow / D) * D;
   const int uri = urho + 4 * D * ujj + C::ROFF;  // raw index of the column's first input
@@ -141,13 +153,17 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // piece j: channel 4q + j; pairs are written after channels 1 and 3.  A piece runs in two parts
   // one MFMA step apart: job_load issues its 7 LDS reads, job_finish transforms (and splits and
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
+  // job index j = 0..3 -> channel piece (a spread lane maps its jobs 0, 1 onto its pair; 2, 3 are empty)
+  auto piece = [&](int j) { return SPREAD && grp == 1 ? 2 * jp + j : j; };
   auto job_load = [&](int rb, int j) {
+    if (SPREAD && grp == 1 && j >= 2) return;
     if (!uok) return;
-    const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + j) * C::RPITCH + uri;
+    const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::RPITCH + uri;
 #pragma unroll
     for (int k = 0; k < 7; ++k) jraw[k] = raw[D * k];
   };
   auto job_finish = [&](int tb, int j) {
+    if (SPREAD && grp == 1 && j >= 2) return;
     if (!uok) return;
     float v[7], t[7];
 #pragma unroll
@@ -162,7 +178,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       for (int k = 0; k < 7; ++k) tkeep[k] = t[k];
       return;
     }
-    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 8 * uq + 4 * (j >> 1);
+    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 8 * uq + 4 * (piece(j) >> 1);
 #pragma unroll
     for (int p = 0; p < kWinoPoints; ++p) {
       unsigned w[NP];
