@@ -99,6 +99,9 @@ struct ResPairArgs {
 bool resblock_pair_supported(int mode, int C, int K, int dil);
 bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster
 void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
+// persistent ping-pong form of the same iteration (kernels_resblock_pp.hip): f16x3 / bf16
+bool resblock_pp_enabled(int mode, int C, int K);
+void launch_resblock_pp(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
 
 // A whole kernel-3 ResBlock1 (three iterations, six convs) in one kernel (kernels_resblock.hip):
 // x stays in registers between iterations (residual), lrelu(x) and xt pass through LDS.

@@ -404,6 +404,10 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
   TTS_REQUIRE(a.c1.cvec == nullptr && a.c2.cvec == nullptr && a.c1.bias && a.c2.bias, 1,
               "resblock pair: biases required, no cond vector (both are staged in LDS)");
   TTS_REQUIRE((int64_t)C * a.c1.Tout * 4 < (int64_t(1) << 31), 3, "resblock pair: plane exceeds 2 GiB");
+  if (resblock_pp_enabled(mode, C, K)) {
+    launch_resblock_pp(mode, a, B, K, C, s);
+    return;
+  }
   if (mode == MATH_FP32_F16X3) launch_pair_s<SchemeH3>(a, B, K, C, s);
   else if (mode == MATH_BF16) launch_pair_s<SchemeB1>(a, B, K, C, s);
   else launch_pair_s<SchemeX6>(a, B, K, C, s);
