@@ -40,6 +40,24 @@ __device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
   return (g * xrows + r) * 8 + 4 * (q ^ ((r >> 3) & 1));
 }
 
+// Max over the 64 lanes of a wave, returned wave-uniform (called with every lane active): DPP
+// row operations (quad swaps, half-row / row mirrors, row broadcasts 15 and 31), a few cycles each,
+// instead of six dependent ds_bpermute round trips.  fmaxf drops NaN like the shuffle form did.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_max_step(float v) {
+  const int o = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false);
+  return fmaxf(v, __builtin_bit_cast(float, o));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = dpp_max_step<0xB1, 0xF>(v);   // quad_perm [1, 0, 3, 2]
+  v = dpp_max_step<0x4E, 0xF>(v);   // quad_perm [2, 3, 0, 1]
+  v = dpp_max_step<0x141, 0xF>(v);  // row_half_mirror: 8-lane halves
+  v = dpp_max_step<0x140, 0xF>(v);  // row_mirror: rows of 16
+  v = dpp_max_step<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v = dpp_max_step<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3: lane 63 holds the max
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 // Conv1d epilogue on a TM x TN grid of 32x32 accumulators (v_mfma_f32_32x32x*):
 // lane holds column (lane&31) and rows (r&3) + 8*(r>>2) + 4*(lane>>5) of each block.
 //   v = act_out(acc + bias[co] [+ cvec[b][co]]) [* mask[b][t]] [+ res]
@@ -52,8 +70,7 @@ __device__ __forceinline__ int xlds_off(int g, int r, int q, int xrows) {
 // wave's max goes to slot blockIdx.x & 63 of its item (fp32 bits order like unsigned integers
 // for non-negative values).  Per item, so an utterance's scaling never depends on its batch.
 __device__ __forceinline__ void publish_amax(unsigned* slots, int b, float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  v = wave_max(v);
   if ((threadIdx.x & 63) == 0) atomicMax(slots + (size_t)b * 64 + (blockIdx.x & 63), __float_as_uint(v));
 }
 
@@ -62,8 +79,7 @@ __device__ __forceinline__ void publish_amax(unsigned* slots, int b, float v) {
 // two slot cache lines serialise in L2 and doubled the Glow gate / update kernels' time.
 __device__ __forceinline__ void publish_amax_block(unsigned* slots, int b, float v) {
   __shared__ float red[4];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  v = wave_max(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0)

@@ -243,8 +243,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
     float tscale = 1.f;
     int et = 0;
     if (H3) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+      tmax = wave_max(tmax);
       if (lane == 0) red[wave] = tmax;
       __syncthreads();
       const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -624,8 +623,7 @@ void resblock3_kernel(ResBlock3Args a) {
   // block max of |v| over this workgroup (f16x3 scale exponent); every wave must call it
   auto tile_exp = [&](float vmax) -> int {
     if (!H3) return 0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+    vmax = wave_max(vmax);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();  // also: every wave is done reading the LDS region
     float mx = red[0];

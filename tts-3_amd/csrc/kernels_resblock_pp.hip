@@ -14,12 +14,13 @@
 // matrix pipe always has one group's MFMAs.  A period has two workgroup barriers:
 //   phase 1   A: convs1(p) MFMAs (the raw window of tile p + 1 is requested PD steps before the
 //                end), lrelu, bias, edge zeros, wave max -> red
-//             B: epilogue of tile p - 2 (bias, residual, MRF sum, statistics, stores)
+//             B: epilogue of tile p - 2 (bias, residual, MRF sum, statistics, stores), then the
+//                first K1 steps of convs2(p - 1)
 //   --- barrier 1 ---
 //   phase 2   A: block max -> xt(p) scale, split xt(p) into LDS buffer p & 1, split the window of
 //                tile p + 1 into X
-//             B: convs2(p - 1) MFMAs from buffer (p - 1) & 1 (its residual requested PD steps
-//                before the end)
+//             B: the other steps of convs2(p - 1) from buffer (p - 1) & 1 (its residual
+//                requested PD steps before the end)
 //   --- barrier 2 ---
 // The HBM requests of a group are issued after its last weight load of the phase (the vector
 // memory counter retires in order: a weight wait behind an HBM load would stall the step loop);
@@ -40,8 +41,14 @@ namespace tts {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifndef PP_ABLATE
+#define PP_ABLATE 0  // diagnostic builds only: 1 = no window loads (stale X), 2 = no epilogue stores
+#endif
 #ifndef PP_BPD
-#define PP_BPD 2  // B-operand LDS reads issued this many steps ahead
+#define PP_BPD 1  // B-operand LDS reads issued this many steps ahead (2 measured no better)
+#endif
+#ifndef PP_K1
+#define PP_K1 0  // convs2 steps in phase 1 (0: NS / 2)
 #endif
 #ifndef PP_PD
 #define PP_PD 4  // weight prefetch distance: each group's MFMA phase runs alone on the matrix pipe
@@ -81,9 +88,13 @@ struct PPCfg {
   static constexpr int LDSB = XB + 2 * TB;    // X + two xt buffers
   static constexpr int UPT = (XROWS * 4 + 255) / 256;  // window units (row, channel quad) per A lane
   static constexpr int NS = NC * K;           // MFMA steps per conv
-  static constexpr int PD = PP_PD;            // weight prefetch distance (steps)
+  static constexpr int PD = PP_PD < NS ? PP_PD : NS - 1;  // weight prefetch distance (steps)
   static_assert(K - 2 < 16, "xt rows");
   static_assert(PD < NS, "prefetch distance");
+  // convs2 steps group B runs in phase 1 (beside group A's convs1), the rest in phase 2; the
+  // residual request (step NS - PD) must fall in phase 2
+  static constexpr int K1A = PP_K1 > 0 ? PP_K1 : NS / 2;
+  static constexpr int K1 = K1A < NS - PD ? K1A : NS - PD;
   static_assert(LDSB <= 160 * 1024 - 1024, "LDS");
 };
 
@@ -284,8 +295,7 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
   };
   auto slot_exp = [&](float m) -> int {
     if (!H3 || !a1.amax_in) return 0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = wave_max(m);
     int e = 0;
     if (m > 0.f && m < INFINITY) {
       int E;
@@ -332,7 +342,7 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
         v = v + rv[n][r];
         if (ZG) v = zdivide ? (zv[n][r] + v) / zdiv : zv[n][r] + v;
         vm = fmaxf(vm, fabsf(v));
-        bstore(rout, v, voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u);
+        if (!(PP_ABLATE & 2)) bstore(rout, v, voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u);
       }
       if (tok) vmax = fmaxf(vmax, vm);
     }
@@ -365,7 +375,7 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
         for (int j = 0; j < BPD; ++j) read_b(smem, P::XSZB, d, j, bq[j]);
         // the next tile's window after the period's last weight load
         auto hook = [&](int s) {
-          if (s == NS - PD) load_window(more ? p + 1 : p);
+          if (!(PP_ABLATE & 1) && s == NS - PD) load_window(more ? p + 1 : p);
         };
 #pragma unroll
         for (int s = 0; s < NS; ++s) step(smem, P::XSZB, d, s, hook);
@@ -388,8 +398,7 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
             tmax = fmaxf(tmax, fabsf(v));
           }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+        tmax = wave_max(tmax);
         if (lane == 0) red[gw] = tmax;
         ex_next = slot_exp(slot_next);
       }
@@ -447,28 +456,35 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
     // ================================ group B: convs2 ================================
     for (int p = 0; p <= nloc + 1; ++p) {
       asm volatile("" : "+v"(lane_off));
+      const bool cur = p >= 1 && p <= nloc;
+      const unsigned char* xt = smem + P::XB + ((p - 1) & 1) * P::TB;
       PPST(0);
-      // ---- phase 1: epilogue of tile p - 2 (group A runs convs1(p)) ----
+      // ---- phase 1: epilogue of tile p - 2, then the first K1 steps of convs2(p - 1)
+      //      (group A runs convs1(p)) ----
       if (p >= 2) {
         b_epilogue(p - 2);
         prefetch_w();
       }
-      PPST(2);
-      lds_barrier();  // -------------------------------------------- barrier 1
-      PPST(3);
-      // ---- phase 2: convs2 of tile p - 1 from xt((p - 1) & 1) (group A writes LDS) ----
-      if (p >= 1 && p <= nloc) {
-        const unsigned char* xt = smem + P::XB + ((p - 1) & 1) * P::TB;
+      if (cur) {
 #pragma unroll
         for (int n = 0; n < TN; ++n) acc[n] = f32x16{};
 #pragma unroll
         for (int j = 0; j < BPD; ++j) read_b(xt, P::TGB, 1, j, bq[j]);
+        auto nohook = [&](int) {};
+#pragma unroll
+        for (int s = 0; s < P::K1; ++s) step(xt, P::TGB, 1, s, nohook);
+      }
+      PPST(2);
+      lds_barrier();  // -------------------------------------------- barrier 1
+      PPST(3);
+      // ---- phase 2: the rest of convs2(p - 1) from buffer (p - 1) & 1 (group A writes LDS) ----
+      if (cur) {
         // the residual after the last weight load; it lands during barrier 2 / the next phase 1
         auto hook = [&](int s) {
           if (s == NS - PD) gather(p - 1, true, false);
         };
 #pragma unroll
-        for (int s = 0; s < NS; ++s) step(xt, P::TGB, 1, s, hook);
+        for (int s = P::K1; s < NS; ++s) step(xt, P::TGB, 1, s, hook);
       }
       PPST(4);
       PPST(6);

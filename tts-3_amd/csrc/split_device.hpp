@@ -80,8 +80,7 @@ struct SchemeB1 {
 __device__ __forceinline__ int amax_exp(const unsigned* slots, int b) {
   if (!slots) return 0;
   float m = __uint_as_float(slots[(size_t)b * 64 + (threadIdx.x & 63)]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  m = wave_max(m);
   int e = 0;
   if (m > 0.f && m < INFINITY) {
     int E;
