@@ -159,6 +159,8 @@ CONVT_CASES = [
     (2, 64, 32, 50, 4),
     (1, 48, 24, 17, 2),   # ragged
     (3, 40, 20, 9, 8),    # ragged
+    (2, 128, 64, 70, 8),  # window-resident x8 form at 128 input channels (2 passes of 256 rows)
+    (3, 256, 128, 129, 8),  # window-resident x8 form: frames across two 64-frame tiles + the pad frame
 ]
 
 

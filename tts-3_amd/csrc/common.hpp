@@ -179,6 +179,9 @@ ConvTile conv1d_split_tile(int mode, int idx);
 int conv1d_split_num_tiles(int mode);
 int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res);
 void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile_idx, hipStream_t s);
+// window-resident form of the x8 ConvTranspose layers (kernels_convT_res.hip)
+bool convT_res_supported(int mode, const Conv1dArgs& a);
+void launch_convT_res(int mode, const Conv1dArgs& a, int B, hipStream_t s);
 // slots[b][0..63] = max |x[b]| over n floats per item (fp32 bits, atomicMax; zero them first)
 // stride: floats between batch items (0 = n, contiguous items)
 void launch_amax(const float* x, int64_t n, int B, unsigned* slots, hipStream_t s, int64_t stride = 0);

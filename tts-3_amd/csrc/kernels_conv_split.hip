@@ -155,6 +155,10 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, 
     const char* e = std::getenv("TTS_MI355X_XCD_REMAP");
     return e ? std::atoi(e) : 0;
   }();
+  if (a.ups > 0 && convT_res_supported(mode, a)) {
+    launch_convT_res(mode, a, B, s);
+    return;
+  }
   Conv1dArgs ar = a;
   const int gy = ceil_div(a.Cout, conv1d_split_tile(mode, tile).BM);
   const int64_t nwg = (int64_t)ceil_div(a.Tout, conv1d_split_tile(mode, tile).BN) * gy * B;
