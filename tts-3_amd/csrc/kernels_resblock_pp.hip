@@ -79,7 +79,12 @@ struct PPCfg {
   static constexpr int RP_BN = RP_W - 2 * LEAD;
   static constexpr int NC = C / 16;           // 16-channel groups
   static constexpr int HMAX = (K - 1) * 5;    // dilation <= 5
-  static constexpr int XROWS = RP_W + HMAX;
+  // window rows: RP_W + HMAX (one per frame), or (V4 form) from the frame rounded down to a
+  // multiple of 4, so that every lane loads 4 aligned frames of one channel with one dwordx4
+  static constexpr int XROWS4 = (RP_W + HMAX + 3 + 3) / 4 * 4;
+  static constexpr int NQ = XROWS4 / 4;                       // frame quads per channel (V4)
+  static constexpr int UPT4 = (NC * 16 * NQ + 255) / 256;    // dwordx4 units per A lane (V4)
+  static constexpr int XROWS = XROWS4;
   static constexpr int XSZB = XROWS * S::ROWB;  // X: one 16-channel group
   static constexpr int TROWS = RP_W + 16;     // xt rows (convs2 reads RP_W + K - 2 at most)
   static constexpr int TGB = TROWS * S::ROWB; // xt: one 16-channel group
@@ -98,7 +103,7 @@ struct PPCfg {
   static_assert(LDSB <= 160 * 1024 - 1024, "LDS");
 };
 
-template <class S, int K, int C, bool ZG>
+template <class S, int K, int C, bool ZG, bool V4>
 __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int ntx, int ntiles) {
   using P = PPCfg<S, K, C>;
   constexpr int NP = S::NP;
@@ -199,57 +204,102 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
   };
 
   // ---- group A: the input window of a tile (raw fp32 in registers, then split into X) ----
+  // V4 (T % 4 == 0): lane unit = (16-channel group, channel, frame quad): one dwordx4 of 4 frames,
+  // stored as 4 rows x 2-byte pieces; X row r holds frame fa + r with fa the window start rounded
+  // down to a multiple of 4, and the MFMA reads shift by roff = start - fa.  Otherwise: unit =
+  // (row, channel quad), 4 dword loads of 4 channels, one u16x4 store per piece.
   const int ta = tid & 255;
-  f32x4 xraw[NC][P::UPT];
+  constexpr int UPW = V4 ? P::UPT4 : NC * P::UPT;
+  f32x4 xraw[UPW];
+  int roff_next = 0;
   auto load_window = [&](int p) {
     const int id = tile_id(p);
     const int b = id / ntx;
     const int tx0 = (id - b * ntx) * RP_BN - P::LEAD;
-    const int XW = RP_W + (K - 1) * d;
     const float* xb = a1.x + (size_t)b * C * T;
+    if constexpr (V4) {
+      const int a0 = tx0 - a1.pad;
+      const int fa = a0 - (((a0 % 4) + 4) % 4);
+      roff_next = a0 - fa;
+      const rsrc_t rx = make_rsrc(xb, (unsigned)C * chb);
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * T, (unsigned)(C - c * 16) * chb);
-#pragma unroll
-      for (int i = 0; i < P::UPT; ++i) {
+      for (int i = 0; i < UPW; ++i) {
         const int u = ta + i * 256;
-        const int q = u & 3, r = u >> 2;
-        const int ts = tx0 - a1.pad + r;
-        const bool ok = r < XW && ts >= 0 && ts < T;
-        // OOB_OFF + 3 * chb stays >= 2^31 (planes < 2 GiB): still out of range.  Laundered: the
-        // compiler otherwise splits the loads into exec-masked branches on vo == OOB_OFF
-        unsigned vo = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+        const int c16 = u & 15, rest = u >> 4;
+        const int g = rest / P::NQ, tq = rest - (rest / P::NQ) * P::NQ;
+        const int ts = fa + 4 * tq;
+        const bool ok = g < NC && ts >= 0 && ts < T;  // whole quads: fa and T are multiples of 4
+        unsigned vo = ok ? (unsigned)(16 * g + c16) * chb + (unsigned)ts * 4u : OOB_OFF;
         asm volatile("" : "+v"(vo));
+        xraw[i] = bload4(rx, vo, 0u);
+      }
+    } else {
+      const int XW = RP_W + (K - 1) * d;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xraw[c][i][j] = bload(rx, vo + (unsigned)j * chb, 0u);
+      for (int c = 0; c < NC; ++c) {
+        const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * T, (unsigned)(C - c * 16) * chb);
+#pragma unroll
+        for (int i = 0; i < P::UPT; ++i) {
+          const int u = ta + i * 256;
+          const int q = u & 3, r = u >> 2;
+          const int ts = tx0 - a1.pad + r;
+          const bool ok = r < XW && ts >= 0 && ts < T;
+          // OOB_OFF + 3 * chb stays >= 2^31 (planes < 2 GiB): still out of range.  Laundered: the
+          // compiler otherwise splits the loads into exec-masked branches on vo == OOB_OFF
+          unsigned vo = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+          asm volatile("" : "+v"(vo));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xraw[c * P::UPT + i][j] = bload(rx, vo + (unsigned)j * chb, 0u);
+        }
       }
     }
   };
   auto store_window = [&](int ex) {
     const float xs = H3 ? ldexpf(1.f, -ex) : 1.f;
-    const int XW = RP_W + (K - 1) * d;
+    if constexpr (V4) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int i = 0; i < P::UPT; ++i) {
+      for (int i = 0; i < UPW; ++i) {
         const int u = ta + i * 256;
-        const int q = u & 3, r = u >> 2;
-        if (r < XW) {
-          u16x4 pv[NP];
+        const int c16 = u & 15, rest = u >> 4;
+        const int g = rest / P::NQ, tq = rest - (rest / P::NQ) * P::NQ;
+        if (g < NC) {
+          unsigned char* dst = smem + g * P::XSZB + (4 * tq) * S::ROWB + 2 * c16;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             unsigned short h[NP];
-            float v = lrelu2(xraw[c][i][j], a1.in_slope);
+            float v = lrelu2(xraw[i][j], a1.in_slope);
             if (H3) v *= xs;
             S::split(v, h);
 #pragma unroll
-            for (int pq = 0; pq < NP; ++pq) pv[pq][j] = h[pq];
+            for (int pq = 0; pq < NP; ++pq) *reinterpret_cast<unsigned short*>(dst + j * S::ROWB + 32 * pq) = h[pq];
           }
-#pragma unroll
-          for (int pq = 0; pq < NP; ++pq)
-            *reinterpret_cast<u16x4*>(smem + c * P::XSZB + r * S::ROWB + 8 * q + 32 * pq) = pv[pq];
         }
       }
+    } else {
+      const int XW = RP_W + (K - 1) * d;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < P::UPT; ++i) {
+          const int u = ta + i * 256;
+          const int q = u & 3, r = u >> 2;
+          if (r < XW) {
+            u16x4 pv[NP];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              unsigned short h[NP];
+              float v = lrelu2(xraw[c * P::UPT + i][j], a1.in_slope);
+              if (H3) v *= xs;
+              S::split(v, h);
+#pragma unroll
+              for (int pq = 0; pq < NP; ++pq) pv[pq][j] = h[pq];
+            }
+#pragma unroll
+            for (int pq = 0; pq < NP; ++pq)
+              *reinterpret_cast<u16x4*>(smem + c * P::XSZB + r * S::ROWB + 8 * q + 32 * pq) = pv[pq];
+          }
+        }
+    }
   };
 
   // ---- group B: epilogue gathers (residual x, MRF z) of tile p and the store ----
@@ -304,9 +354,11 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
     }
     return __builtin_amdgcn_readfirstlane(e);
   };
+  int roff = 0;  // X row of the window's first frame (V4)
   if (grp == 0 && nloc > 0) {
     load_window(0);
     store_window(slot_exp(slot_load(0)));
+    roff = roff_next;
   }
   prefetch_w();
   __syncthreads();
@@ -372,13 +424,13 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
 #pragma unroll
         for (int n = 0; n < TN; ++n) acc[n] = f32x16{};
 #pragma unroll
-        for (int j = 0; j < BPD; ++j) read_b(smem, P::XSZB, d, j, bq[j]);
+        for (int j = 0; j < BPD; ++j) read_b(smem + roff * S::ROWB, P::XSZB, d, j, bq[j]);
         // the next tile's window after the period's last weight load
         auto hook = [&](int s) {
           if (!(PP_ABLATE & 1) && s == NS - PD) load_window(more ? p + 1 : p);
         };
 #pragma unroll
-        for (int s = 0; s < NS; ++s) step(smem, P::XSZB, d, s, hook);
+        for (int s = 0; s < NS; ++s) step(smem + roff * S::ROWB, P::XSZB, d, s, hook);
         PPST(1);
         // lrelu(acc * 2^(ex + w_exp) + bias), zero outside [0, T) (convs2's zero padding)
         const float sc1 = H3 ? ldexpf(1.f, ex + a1.w_exp) : 1.f;
@@ -444,6 +496,7 @@ __global__ __launch_bounds__(512) void resblock_pp_kernel(ResPairArgs pa, int nt
         if (more) {
           ex = ex_next;
           store_window(ex);
+          roff = roff_next;
           PPST(5);
           prefetch_w();
         }
@@ -516,10 +569,19 @@ void launch_pp_t(const ResPairArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(nt < (int64_t(1) << 30), 3, "resblock pair: too many tiles");
   const int ntiles = (int)nt;
   const int grid = std::min(ntiles, num_cus());
-  if (a.c2.zmode >= 2)
-    hipLaunchKernelGGL((resblock_pp_kernel<S, K, C, true>), dim3(grid), dim3(512), 0, s, a, ntx, ntiles);
-  else
-    hipLaunchKernelGGL((resblock_pp_kernel<S, K, C, false>), dim3(grid), dim3(512), 0, s, a, ntx, ntiles);
+  // V4 window loads need whole frame quads: T % 4 == 0 (every HiFiGAN stage at T' % 4 == 0... and
+  // the bench shapes); TTS_MI355X_PP_V4=0 keeps the dword form (A/B runs)
+  static const bool v4on = [] {
+    const char* e = std::getenv("TTS_MI355X_PP_V4");
+    return !(e && e[0] == '0');
+  }();
+  const bool v4 = v4on && a.c1.Tout % 4 == 0;
+  const bool zg = a.c2.zmode >= 2;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, a, ntx, ntiles); };
+  if (zg && v4) go(resblock_pp_kernel<S, K, C, true, true>);
+  else if (zg) go(resblock_pp_kernel<S, K, C, true, false>);
+  else if (v4) go(resblock_pp_kernel<S, K, C, false, true>);
+  else go(resblock_pp_kernel<S, K, C, false, false>);
 }
 
 template <class S, int K>
