@@ -464,7 +464,7 @@ void resblock3_kernel(ResBlock3Args a) {
   constexpr int PD = 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
   constexpr int NT = P::NT;
-  __shared__ float red[P::NW];
+  __shared__ float red[2][P::NW];  // double-buffered: consecutive tile_exp calls use different halves
   __shared__ float bsm[6 * C];  // the six conv biases (read by every epilogue: LDS, not L2, latency)
 
   const int tid = threadIdx.x;
@@ -620,16 +620,19 @@ void resblock3_kernel(ResBlock3Args a) {
       }
     }
   };
-  // block max of |v| over this workgroup (f16x3 scale exponent); every wave must call it
+  // block max of |v| over this workgroup (f16x3 scale exponent); every wave must call it.  The
+  // red halves alternate per call, and the store_pieces barrier between two calls separates a
+  // half's reads from its next writes, so one barrier per call suffices
+  int red_half = 0;
   auto tile_exp = [&](float vmax) -> int {
     if (!H3) return 0;
     vmax = wave_max(vmax);
-    if (lane == 0) red[wave] = vmax;
+    if (lane == 0) red[red_half][wave] = vmax;
     __syncthreads();  // also: every wave is done reading the LDS region
-    float mx = red[0];
+    float mx = red[red_half][0];
 #pragma unroll
-    for (int w = 1; w < P::NW; ++w) mx = fmaxf(mx, red[w]);
-    __syncthreads();  // red[] is reused by the next call
+    for (int w = 1; w < P::NW; ++w) mx = fmaxf(mx, red[red_half][w]);
+    red_half ^= 1;
     int e = 0;
     if (mx > 0.f && mx < INFINITY) {
       int E;
@@ -638,6 +641,7 @@ void resblock3_kernel(ResBlock3Args a) {
     }
     return e;
   };
+
   // acc-layout values (already zeroed where invalid) -> split pieces at LDS row column + roff;
   // rows of the region outside [roff, roff + RP_W) are zeroed
   auto store_pieces = [&](int roff, float scale) {
