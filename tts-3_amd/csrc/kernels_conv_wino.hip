@@ -31,7 +31,16 @@ void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
     const char* e = std::getenv("TTS_MI355X_WINO8");
     return !(e && e[0] == '0');
   }();
-  if (w8 && a.Tin % 4 == 0) wino8_detail::launch_s<SchemeH3>(a, B, K, s);
+  // TTS_MI355X_WINO_XCD=1: the m-blocks of a column tile on one XCD (8-wave form, Cout > 128)
+  static const bool xcd = [] {
+    const char* e = std::getenv("TTS_MI355X_WINO_XCD");
+    return e && e[0] == '1';
+  }();
+  if (w8 && a.Tin % 4 == 0) {
+    Conv1dArgs ar = a;
+    ar.xcd_remap = xcd && a.Cout > 128 ? 2 : 0;  // wino8 launch_d checks the grid divisibility
+    wino8_detail::launch_s<SchemeH3>(ar, B, K, s);
+  }
   else wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
