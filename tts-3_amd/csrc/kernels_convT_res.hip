@@ -20,6 +20,10 @@
 
 namespace tts {
 
+#ifndef CONVT_RES_PD
+#define CONVT_RES_PD 3  // weight prefetch distance (steps)
+#endif
+
 template <class S, int NG>
 struct ConvTResCfg {
   static constexpr int BN = 64;                // frames per workgroup (2 column blocks per wave)
@@ -29,7 +33,7 @@ struct ConvTResCfg {
   static constexpr int UNITS = NG * XROWS * 4;  // staging units (group, row, channel quad)
   static constexpr int UPT = (UNITS + 511) / 512;
   static constexpr int NS = NG * 2;            // MFMA steps (group, tap)
-  static constexpr int PD = 3;                 // weight prefetch distance
+  static constexpr int PD = CONVT_RES_PD;      // weight prefetch distance
   static_assert(LDSB <= 96 * 1024, "LDS window");
 };
 
