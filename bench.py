@@ -12,11 +12,14 @@ utterances at N=8).  The compute-only step (each rank on its resident shard) and
 gather times are reported beside it.
 
 Prints ONE JSON line (rank 0) with the driver contract fields plus:
-  roofline     : the dominant kernel family's algorithmic FLOP/s (hipEvent-timed inside one
-                 profiled forward, on the stream the kernels run on) vs the 157.3 TF fp32 peak
+  roofline     : the dominant kernel family's executed MFMA FLOP/s (the products its algorithm
+                 issues: Winograd F(4,4) point products, x3 fp16 products per fp32 MAC in f16x3),
+                 timed by a hipEvent pair per launch inside one profiled forward on the stream the
+                 kernels run on, against the dense peak of the matrix pipe it uses (fp16 / bf16
+                 2.5 PF, fp32 157.3 TF); the direct-conv-equivalent rate is reported beside it
   cpu_baseline : the CPU oracle (oracle/hifigan_ref.py, torch.nn.functional fp32, the same
-                 ATen kernels as the reference) on the first utterances of the bench's own mel
-                 batch (median of 3 runs after one warm-up), rank 0 at N=1 only
+                 ATen kernels as the reference) on the bench's whole [32,80,1024] mel batch
+                 (median of 3 runs after one warm-up), rank 0 at N=1 only
   build        : provenance of the loaded library (source hash stamped at build time, .so sha256)
 """
 from __future__ import annotations
@@ -39,7 +42,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA
+# MFMA products each mode issues per fp32 multiply-accumulate, and the dense peak of the pipe
+PRODUCTS = {"fp32": 1, "fp32x6": 6, "f16x3": 3, "bf16": 1}
+PIPE_PEAK = {"fp32": FP32_PEAK_TFLOPS, "fp32x6": BF16_PEAK_TFLOPS, "f16x3": BF16_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
+PIPE_BASIS = {"fp32": "fp32 MFMA dense 157.3 TF", "fp32x6": "bf16 MFMA dense 2.5 PF",
+              "f16x3": "fp16 MFMA dense 2.5 PF", "bf16": "bf16 MFMA dense 2.5 PF"}
 # ceiling of each math mode in algorithmic fp32 FLOP/s: fp32x6 issues 6 bf16 MFMA products
 # per fp32 multiply-accumulate, f16x3 3 fp16 products (same MFMA rate as bf16); see
 # include/tts_mi355x.h TTS_MATH_*
@@ -81,7 +89,8 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r03.json"))
     p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r03.json"),
                    help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
-    p.add_argument("--cpu-utts", type=int, default=2, help="utterances of the bench batch the CPU baseline vocodes")
+    p.add_argument("--cpu-utts", type=int, default=0,
+                   help="utterances of the bench batch the CPU baseline vocodes (0: the whole batch)")
     p.add_argument("--comm-timeout", type=float, default=300.0, help="collective timeout (s), fail-fast")
     p.add_argument("--rank-timeout", type=float, default=1500.0,
                    help="a rank that runs longer than this dumps its stack and exits (hung peer)")
@@ -129,16 +138,14 @@ def dominant_kernel(rows):
     return name, f, fam
 
 
-def winograd_fields(fam_name: str, achieved: float, peak: float) -> dict:
-    """The Winograd F(4,4) convs ("mrf_wino_k<K>_c<C>", wino8_kernel.hpp) compute the same outputs
-    with 7*ceil(K/4)/4 instead of K products per (output, co, ci): `achieved` stays the algorithmic
-    (direct-conv) FLOP rate, and the MFMA work actually issued is reported next to it."""
+def algorithm_ratio(fam_name: str):
+    """Multiplies the family's algorithm issues per direct-conv multiply: the Winograd F(4,4)
+    convs ("mrf_wino_k<K>_c<C>", wino8_kernel.hpp) take 7*ceil(K/4)/4 instead of K products per
+    (output, co, ci); every other kernel is a direct conv (1)."""
     if not fam_name.startswith("mrf_wino_k"):
-        return {"algorithm": "direct"}
+        return "direct", 1.0
     K = int(fam_name.split("_k")[1].split("_")[0])
-    ratio = 7 * ((K + 3) // 4) / 4 / K
-    return {"algorithm": "winograd F(4,4)", "mfma_products_per_direct": ratio,
-            "mfma_executed_tflops": achieved * ratio, "mfma_executed_frac": achieved * ratio / peak}
+    return "winograd F(4,4)", 7 * ((K + 3) // 4) / 4 / K
 
 
 def cpu_baseline(mel, n_utts: int, pad: int = 5):
@@ -156,7 +163,7 @@ def cpu_baseline(mel, n_utts: int, pad: int = 5):
     cfg = dict(in_channels=80, out_channels=1, **HIFIGAN_V1)
     sd = synthetic.hifigan_state_dict(**cfg, seed=1234, weight_norm=False)
     sd = {k: v.float() for k, v in sd.items()}
-    x = mel[:n_utts].cpu().contiguous()
+    x = (mel[:n_utts] if n_utts > 0 else mel).cpu().contiguous()
     B, _, T = x.shape
     runs = []
     with torch.no_grad():
@@ -623,9 +630,12 @@ def main():
     if os.environ.get("TTS_FORWARD_NAMES") and rank == 0:  # launch sequence for scripts/traffic_from_pmc.py
         json.dump([r["name"] for r in rows], open(os.environ["TTS_FORWARD_NAMES"], "w"))
     fam_name, fam, fams = dominant_kernel(rows)
-    per_launch_flops = fam["flops"] / fam["n"]
+    per_launch_flops = fam["flops"] / fam["n"]  # direct-conv FLOPs of one launch (2 per MAC)
     avg_ms = fam["ms"] / fam["n"]
-    achieved = per_launch_flops / (avg_ms / 1e3) / 1e12
+    direct_tflops = per_launch_flops / (avg_ms / 1e3) / 1e12
+    algo, ratio = algorithm_ratio(fam_name)
+    exec_flops = per_launch_flops * ratio * PRODUCTS[a.math_mode]  # MFMA FLOPs the launch issues
+    achieved = exec_flops / (avg_ms / 1e3) / 1e12
     total_flops = sum(r["flops"] for r in rows)
     traffic = None
     fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r03.json)
@@ -691,18 +701,33 @@ def main():
                 "kernel": fam_name,
                 "launches_per_step": fam["n"],
                 "achieved": achieved,
-                "peak": MODE_PEAK[a.math_mode],
-                "peak_basis": PEAK_BASIS[a.math_mode],
+                "peak": PIPE_PEAK[a.math_mode],
+                "peak_basis": PIPE_BASIS[a.math_mode],
                 "unit": "TFLOP/s",
-                "frac": achieved / MODE_PEAK[a.math_mode],
+                "frac": achieved / PIPE_PEAK[a.math_mode],
                 "traffic": traffic,
-                "flops_per_launch": per_launch_flops,
+                "achieved_basis": (f"MFMA FLOPs the launch issues ({algo}: {ratio:.4f} products per direct-conv "
+                                   f"multiply, x{PRODUCTS[a.math_mode]} {a.math_mode} products per fp32 MAC) / "
+                                   "avg launch time"),
+                "mfma_flops_per_launch": exec_flops,
+                "algorithm": algo,
+                "products_per_direct_multiply": ratio,
                 "avg_launch_ms": avg_ms,
-                **winograd_fields(fam_name, achieved, MODE_PEAK[a.math_mode]),
+                "avg_launch_ms_source": ("hipEvent pair around every launch of one profiled forward (serialised "
+                                         "launches, not the timed steps)"),
+                # the same launch as a direct conv's FLOP rate, against the mode's fp32 ceiling and
+                # BASELINE.md's fp32 basis (a Winograd kernel's saving shows up here as > MFMA rate)
+                "direct_conv_flops_per_launch": per_launch_flops,
+                "direct_equivalent_tflops": direct_tflops,
+                "direct_equivalent_frac_of_mode_ceiling": direct_tflops / MODE_PEAK[a.math_mode],
+                "mode_ceiling_basis": PEAK_BASIS[a.math_mode],
+                "direct_equivalent_vs_fp32_peak": direct_tflops / FP32_PEAK_TFLOPS,
                 **busy,
             },
             "hbm_roofline_step": hbm,
             "kernel_breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1]["ms"])},
+            "kernel_breakdown_source": ("one profiled forward: a hipEvent pair around every launch serialises them, "
+                                        "so the families sum above ms_per_step"),
             "cpu_baseline": cpu,
             "alt_math_mode": alt,
             "glow_decoder": glow,

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == 111
+    assert N.lib().tts_abi_version() == N.ABI_VERSION == 111
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -48,6 +48,7 @@ def test_library_built_from_these_sources():
     build fails here, before any GPU run uses it)."""
     info = N.build_info()
     assert info["target"] == "gfx950"
+    assert info["defs"] == "none", f"the in-tree library is a variant build ({info['defs']})"
     assert info["src"] == N.source_hash(), (
         f"libtts_mi355x.so was built from other sources (src={info['src']}, tree={N.source_hash()}): "
         "rebuild with make -C tts-3_amd")
@@ -133,6 +134,44 @@ def test_setup_generator_and_gan_surface(tmp_path):
     assert np.array_equal(w[0], hifigan_ref.fold_weight_norm(sd, torch.float32)["conv_pre.weight"].numpy())
     with pytest.raises(NotImplementedError):
         setup_generator({**cfg, "generator_model": "melgan_generator"})
+
+
+def test_setup_generator_selects_math_mode(monkeypatch):
+    """The fp32-faithful fast mode is the drop-in default, and a config can pick another one
+    without code edits (generator_model_params, a top-level field, or the environment)."""
+    monkeypatch.delenv("TTS_MI355X_MATH_MODE", raising=False)
+    cfg = {"generator_model": "hifigan_generator", "audio": {"num_mels": 80},
+           "generator_model_params": dict(HIFIGAN_V1)}
+    g = setup_generator(cfg)
+    assert g.math_mode == "f16x3" and g._cfg.math_mode == N.MATH_MODES["f16x3"]
+    assert GAN(cfg).model_g.math_mode == "f16x3"
+    assert HifiganGenerator(**V1).math_mode == "f16x3"
+    assert Decoder(80, 192, 5, 1, 12, 4).math_mode == "f16x3"
+    g = setup_generator({**cfg, "generator_model_params": dict(HIFIGAN_V1, math_mode="fp32")})
+    assert g.math_mode == "fp32" and g._cfg.math_mode == 0
+    g = setup_generator({**cfg, "math_mode": "fp32x6"})
+    assert g._cfg.math_mode == N.MATH_MODES["fp32x6"]
+    monkeypatch.setenv("TTS_MI355X_MATH_MODE", "fp32")
+    assert setup_generator(cfg)._cfg.math_mode == 0
+    monkeypatch.setenv("TTS_MI355X_MATH_MODE", "bf16")  # lower precision: explicit only
+    with pytest.raises(ValueError, match="not fp32-faithful"):
+        setup_generator(cfg)
+    monkeypatch.setenv("TTS_MI355X_MATH_MODE", "tf32")
+    with pytest.raises(ValueError, match="TTS_MI355X_MATH_MODE"):
+        HifiganGenerator(**V1)
+
+
+def test_lib_refuses_other_abi_revision(monkeypatch):
+    """lib() checks tts_abi_version() before binding: a library of another revision would take
+    pointers where it expects sizes."""
+    lib = N.lib()
+    assert lib.tts_abi_version() == N.ABI_VERSION
+    monkeypatch.setattr(N, "_lib", None)
+    monkeypatch.setattr(N, "ABI_VERSION", N.ABI_VERSION + 1)
+    with pytest.raises(RuntimeError, match="C-ABI"):
+        N.lib()
+    monkeypatch.setattr(N, "ABI_VERSION", N.ABI_VERSION - 1)
+    assert N.lib() is not None
 
 
 def test_hifigan_generator_load_checkpoint(tmp_path):

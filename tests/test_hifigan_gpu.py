@@ -5,12 +5,13 @@
 * the whole generator vs the reference's own outputs (tests/golden, fp64 anchor);
 * at the benchmark size (B=32 x 1024 frames) the size-independent properties: finite,
   |y| <= 1, batch-invariance (each utterance bit-identical to running it alone),
-  run-to-run determinism, and one utterance vs the fp32 CPU oracle.
+  run-to-run determinism, and four utterances vs the fp64 CPU oracle.
 
 fp32-faithful gates (tests/_util.py): rel-RMS <= 5e-6 and max|d| <= 1e-5 on waveforms (1e-4 on
 single-op outputs) against the fp64 reference; bf16: SURVEY.md §8c's 3e-2.
 """
 import ctypes
+import functools
 
 import numpy as np
 import pytest
@@ -296,8 +297,20 @@ def test_benchmark_size_properties(cuda_device, mode):
     for i in (0, 17, 31):
         single = g.inference(mel[i : i + 1])
         assert torch.equal(single[0], out[i]), f"batch invariance, item {i}"
-    ref = hifigan_ref.hifigan_forward(sd, mel[17:18].cpu(), pad=5, dtype=torch.float64, **V1)
-    assert_close_fp32(out[17:18].cpu(), ref, "B=32 item 17 vs fp64 oracle", **tol(mode))
+    # f16x3 takes a power-of-two scale per utterance and plane, so each row's arithmetic differs:
+    # four rows (first, two inner, last) against the fp64 oracle, computed once for all modes
+    for i in BENCH_ORACLE_ROWS:
+        assert_close_fp32(out[i : i + 1].cpu(), _bench_row_oracle(i), f"B=32 item {i} vs fp64 oracle", **tol(mode))
+
+
+BENCH_ORACLE_ROWS = (0, 9, 17, 31)
+
+
+@functools.lru_cache(maxsize=None)
+def _bench_row_oracle(i):
+    sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
+    mel = synthetic.mel(32, 1024, seed=0)[i : i + 1]
+    return hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
 
 
 def test_split_modes_accuracy_not_worse_than_fp32(cuda_device, monkeypatch):
@@ -431,6 +444,26 @@ def test_windowed_forward_matches_plain(cuda_device, monkeypatch, mode):
         assert torch.equal(outs["0"], outs["37"])
     ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
     assert_close_fp32(outs["37"], ref, f"windowed ({mode})", **tol(mode))
+
+
+@pytest.mark.parametrize("name", ["hifigan_small_rb2_b2_t16"])
+def test_windowed_halo_other_topologies(cuda_device, monkeypatch, name):
+    """The window halo (Hifigan::window_halo, the generator's receptive-field radius) for the
+    other golden topology (v3-like: ResBlock2, x8 x8 x4 upsampling, dilation up to 12): 7-frame payloads
+    must give the plain forward's output bit for bit in fp32, which only holds when every payload
+    sample's whole receptive field lies inside its window."""
+    hit = [h for h in HIFI if h[0] == name]
+    if not hit:
+        pytest.skip(f"golden {name} absent")
+    _, meta, _ = hit[0]
+    cfg = meta["config"]
+    mel = synthetic.mel(2, 57, channels=cfg.get("in_channels", 80), seed=95)
+    outs = {}
+    for frames in ("0", "7"):
+        monkeypatch.setenv("TTS_MI355X_WINDOW_FRAMES", frames)
+        g = build(cfg, meta["seed"], cuda_device, "fp32")
+        outs[frames] = g.inference(mel.to(cuda_device)).cpu()
+    assert torch.equal(outs["0"], outs["7"])
 
 
 @pytest.mark.slow

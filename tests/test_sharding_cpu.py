@@ -44,11 +44,17 @@ def _worker(rank, world, port, n, T, q):
         # per-utterance "vocoder": output length differs from the input (x256 like HiFiGAN)
         wav = shard.sum(1, keepdim=True).repeat_interleave(4, dim=2)
         out = gather_batch(wav, n)
+        # a caller's non-contiguous `out` and an fp64 `full`: handled on the root,
+        # without failing inside the collective
+        full64 = full.double() if rank == 0 else None
+        ok_scatter = ok_scatter and torch.equal(scatter_batch(full64, n, (3, T), torch.device("cpu")), expect)
+        strided = torch.empty(n, 1, 8 * T).as_strided((n, 1, 4 * T), (8 * T, 8 * T, 2)) if rank == 0 else None
+        out2 = gather_batch(wav, n, out=strided)
         if rank == 0:
             ref = torch.arange(n * 3 * T, dtype=torch.float32).view(n, 3, T).sum(1, keepdim=True).repeat_interleave(4, 2)
-            q.put((rank, ok_scatter, torch.equal(out, ref)))
+            q.put((rank, ok_scatter, torch.equal(out, ref) and out2 is strided and torch.equal(strided, ref)))
         else:
-            q.put((rank, ok_scatter, out is None))
+            q.put((rank, ok_scatter, out is None and out2 is None))
     finally:
         dist.destroy_process_group()
 

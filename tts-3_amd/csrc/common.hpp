@@ -67,7 +67,6 @@ struct Conv1dArgs {
   int64_t o_bstride;     // floats between batch items of res / y / z (0 = Cout*Tout)
   int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
   int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
-  int xcd_remap;         // split kernels: XCD-aware tile order (set by launch_conv1d_split)
   // split tile kSplitGateTile only: the WaveNet gate fused into the epilogue (wavenet.py:6-13).
   // gate = H: the packed rows interleave 64-row blocks of the tanh half (rows [0, H)) and the
   // sigmoid half (rows [H, 2H)) (gate_row_order); y receives acts [B][H][Tout] =
@@ -99,9 +98,6 @@ struct ResPairArgs {
 bool resblock_pair_supported(int mode, int C, int K, int dil);
 bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster
 void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
-// persistent ping-pong form of the same iteration (kernels_resblock_pp.hip): f16x3 / bf16
-bool resblock_pp_enabled(int mode, int C, int K);
-void launch_resblock_pp(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
 
 // A whole kernel-3 ResBlock1 (three iterations, six convs) in one kernel (kernels_resblock.hip):
 // x stays in registers between iterations (residual), lrelu(x) and xt pass through LDS.

@@ -158,91 +158,6 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
 }
 
-// Software-pipelined form (resblock_pair_kernel at 64 channels, where the registers allow it:
-// two blocks of gathers live at once, +34 VGPRs, same occupancy; in the split conv kernels it
-// cost a wave per SIMD).
-template <int TM, int TN, bool RES, int ZM, bool AMAX>
-__device__ __forceinline__ void conv_epilogue_pipe_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
-                                                   int tbase, int cobase, int lane, int tend,
-                                                   const float* sbias, int sbase) {
-  const int half = lane >> 5;
-  const int l32 = lane & 31;
-  const int Cout = a.Cout;
-  const int Tout = a.Tout;
-  const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;  // bytes of one batch item
-  const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
-  const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
-  const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
-  const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
-  const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
-                               a.cvec ? (unsigned)Cout * 4u : 0u);
-  const rsrc_t rmask = make_rsrc(a.mask ? a.mask + (size_t)b * Tout : a.bias, a.mask ? (unsigned)Tout * 4u : 0u);
-  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)Cout * 4u);
-  const bool has_mask = a.mask != nullptr;
-  const bool mask_res = RES && a.mask_res && has_mask;
-  const float oslope = a.out_slope;
-  const float zdiv = a.zdiv;
-  const unsigned rowb = (unsigned)Tout * 4u;
-  float vmax = 0.f;  // AMAX: max |stored value|
-  // Every range-checked offset is in the per-lane voffset (lane row cobase + m*32 + 4*half, column
-  // t; register r adds row (r&3) + 8*(r>>2)); an absent cvec reads 0 through a 0-byte descriptor.
-  // The 32x32 blocks are software-pipelined: block i+1's reads (residual, MRF sum, mask) are issued
-  // before block i's stores, so the tile pays one memory latency instead of one per block (a read
-  // issued after a store would wait for the store in the in-order vmcnt).  Each element is read
-  // and written by the same lane in the same block, so the in-place residual / z stay exact.
-  float bv[TM][16];
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const unsigned co = (unsigned)(cobase + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half);
-      bv[m][r] = sbias ? sbias[(int)co - sbase] : bload(rbias, co * 4u, 0u) + bload(rcv, co * 4u, 0u);
-    }
-  constexpr int NB = TM * TN;
-  float rv[2][16], zv[2][16], mvb[2];
-  unsigned vob[2];
-  bool tokb[2];
-  auto gather = [&](int blk, int sl) {
-    const int m = blk / TN, n = blk % TN;
-    const int t = tbase + n * 32 + l32;
-    const int row0 = cobase + m * 32 + 4 * half;
-    // rows >= Cout land past the plane through the row term; columns >= min(Tout, tend) are OOB
-    const bool tok = t < Tout && t < tend;
-    const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-    tokb[sl] = tok;
-    vob[sl] = voff;
-    mvb[sl] = has_mask ? bload(rmask, (tok ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const unsigned vo = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-      if (RES) rv[sl][r] = bload(rres, vo, 0u);
-      if (ZM >= 2) zv[sl][r] = bload(rz, vo, 0u);
-    }
-  };
-  gather(0, 0);
-#pragma unroll
-  for (int blk = 0; blk < NB; ++blk) {
-    const int sl = blk & 1;
-    const int m = blk / TN, n = blk % TN;
-    if (blk + 1 < NB) gather(blk + 1, sl ^ 1);
-    const float mv = mvb[sl];
-    const float mv2 = mask_res ? mv : 1.f;  // (res + v) * mask for the VITS coupling update
-    float vm = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float v = (acc[m][n][r] + bv[m][r]) * mv;  // mv = 1 without a mask (exact)
-      v = lrelu2(v, oslope);
-      if (RES) v = (v + rv[sl][r]) * mv2;  // mv2 = 1 unless mask_res (exact)
-      if (ZM == 2) v = zv[sl][r] + v;
-      if (ZM == 3) v = (zv[sl][r] + v) / zdiv;
-      if (AMAX) vm = fmaxf(vm, fabsf(v));  // rows >= Cout hold exact zeros
-      bstore(rout, v, vob[sl] + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u);
-    }
-    if (AMAX && tokb[sl]) vmax = fmaxf(vmax, vm);
-  }
-  if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
-}
-
 // Polyphase ConvTranspose1d epilogue (Conv1dArgs::ups = U): row rho = co*U + s, column frame m
 // -> y[b][co][U*m + s - U/2].  For U = 8 a lane's registers r = 4i..4i+3 hold the phases
 // 4*half .. 4*half+3 of one channel, i.e. 4 consecutive samples.
@@ -342,18 +257,14 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 
 // The per-element options are template parameters (one uniform dispatch per tile), so the
 // unrolled epilogue carries no per-element branches.
-template <int TM, int TN, bool AMAX = false, bool PIPE = false>
+template <int TM, int TN, bool AMAX = false>
 __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
                                               int tbase, int cobase, int lane, int tend = 0x7fffffff,
                                               const float* sbias = nullptr, int sbase = 0) {
   // copy the argument block: a store through `out` could alias it in the compiler's view
   const Conv1dArgs a = args;
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
-#define TTS_EPI(RES, ZM)                                                                  \
-  do {                                                                                    \
-    if (PIPE) conv_epilogue_pipe_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase); \
-    else conv_epilogue_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase); \
-  } while (0)
+#define TTS_EPI(RES, ZM) conv_epilogue_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase)
   if (a.res) {
     if (zm == 0) TTS_EPI(true, 0);
     else if (zm == 2) TTS_EPI(true, 2);

@@ -9,12 +9,6 @@
 namespace tts {
 
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil) {
-  static const int forced = [] {
-    const char* e = std::getenv("TTS_MI355X_FLOW_TILE");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (is_split_mode(mode) && forced >= 0 && forced < conv_num_tiles(mode) && (K - 1) * dil <= (K - 1) * 5)
-    return forced;
   return conv_tile_for(mode, Cout, K, Cin, dil, false);
 }
 

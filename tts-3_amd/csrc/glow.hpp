@@ -32,9 +32,8 @@ void launch_glow_squeeze(const float* x, const float* mask, float* xs, float* ms
 void launch_glow_unsqueeze(const float* xs, const float* msq, float* y, int B, int C, int Th, int nsq,
                            hipStream_t s);
 // amax: [B][64] max-abs slots of the output (f16x3 statistics of the next conv's input), or nullptr
-// Conv tile of the Glow / VITS flow convs (glow.cpp): the flows' column counts (B x T/2) are
-// small, so the split modes may take a smaller tile to fill the chip; TTS_MI355X_FLOW_TILE=<idx>
-// overrides it (A/B runs).
+// Conv tile of the Glow / VITS flow convs (glow.cpp): the plain per-shape table (smaller tiles for
+// the flows' short column counts measured slower).
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil);
 // Whether a WN in_layer (H -> 2H, kernel K, dilation dil) runs with the gate fused into its conv
 // epilogue (kSplitGateTile): split modes, H % 64 == 0, K in {3, 5, 7}, the tile's halo, and

@@ -102,12 +102,9 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   // 1) describe layers, 2) size the arena, 3) pack on host, 4) one upload.
   const int C0 = cfg_.upsample_initial_channel;
   const int mode = cfg_.math_mode;
-  // TTS_MI355X_NO_PAIR_FUSION=1 keeps every resblock conv a separate launch (A/B measurements);
-  // TTS_MI355X_PAIR_FUSION=all fuses every supported iteration (not only the measured-faster ones)
+  // TTS_MI355X_NO_PAIR_FUSION=1 keeps every resblock conv a separate launch (the tests' reference arm)
   const char* nf = std::getenv("TTS_MI355X_NO_PAIR_FUSION");
   const bool pair_fusion = !(nf && nf[0] == '1');
-  const char* fa = std::getenv("TTS_MI355X_PAIR_FUSION");
-  const bool fuse_all = fa && std::string(fa) == "all";
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
@@ -186,7 +183,7 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
             // ceil(K/4) steps) must take the per-conv path
             tiles_ok = tiles_ok && !t.WINO && t.CK % 16 == 0 && ch % t.CK == 0 && ch % t.BM == 0;
             rb.fused = rb.fused && !t.WINO && t.CK == 16 && ceil_div(ch, t.BM) * t.BM == ch &&
-                       (fuse_all ? resblock_pair_supported(mode, ch, k, dil) : resblock_pair_preferred(mode, ch, k, dil));
+                       resblock_pair_preferred(mode, ch, k, dil);
           }
         }
         rb.fused3 = pair_fusion && tiles_ok;
@@ -341,12 +338,13 @@ int64_t Hifigan::cond_floats(int B) const {
 // ---------------------------------------------------------------------------------------
 int Hifigan::window_halo() const {
   // receptive-field radius of one output sample, in mel frames: conv_pre (k7), then per stage the
-  // polyphase ConvTranspose (taps x[m-1], x[m]: one input sample) and the widest MRF branch
-  // (ResBlock1: sum_m (k-1)/2 * (d_m + 1); ResBlock2: sum_m (k-1)/2 * d_m samples at the
-  // stage's rate), then conv_post (k7) at the output rate
+  // polyphase ConvTranspose (output n reads x[m-1] and x[m], m = floor((n + U/2) / U): up to 1.5
+  // input samples from n / U) and the widest MRF branch (ResBlock1: sum_m (k-1)/2 * (d_m + 1);
+  // ResBlock2: sum_m (k-1)/2 * d_m samples at the stage's rate), then conv_post (k7) at the
+  // output rate.  The +2 frames are slack (tests/test_hifigan_gpu.py probes the radius)
   double r = 3.0, rate = 1.0;
   for (int i = 0; i < cfg_.num_upsamples; ++i) {
-    r += 1.0 / rate;
+    r += 1.5 / rate;
     rate *= cfg_.upsample_factors[i];
     int widest = 0;
     for (int j = 0; j < cfg_.num_kernels; ++j) {

@@ -704,23 +704,12 @@ void launch_convT(const ConvTArgs& a, int B, int U, int tile, hipStream_t s) {
   TTS_HIP_CHECK(hipGetLastError());
 }
 
-namespace {
-// TTS_MI355X_POST4=0 keeps the LDS-window conv_post for every T (A/B runs)
-bool post4_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("TTS_MI355X_POST4");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-}  // namespace
-
 void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.Cin >= 1 && a.Cin <= POST_MAXC, 3, "conv_post: more than 64 input channels");
   TTS_REQUIRE((int64_t)a.Cin * a.T * 4 < (int64_t(1) << 31), 3, "conv_post: channel plane exceeds 2 GiB");
   dim3 grid(ceil_div(a.T, POST_T), B);
   // the vector form needs 16-byte aligned rows (T % 4 == 0) and plane bases
-  const bool vec = a.T % 4 == 0 && ((uintptr_t)a.z & 15) == 0 && ((uintptr_t)a.y & 15) == 0 && post4_enabled();
+  const bool vec = a.T % 4 == 0 && ((uintptr_t)a.z & 15) == 0 && ((uintptr_t)a.y & 15) == 0;
   if (vec) hipLaunchKernelGGL(conv_post4_kernel, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), 0, s, a);
   TTS_HIP_CHECK(hipGetLastError());

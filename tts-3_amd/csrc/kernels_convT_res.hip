@@ -20,9 +20,6 @@
 
 namespace tts {
 
-#ifndef CONVT_RES_PD
-#define CONVT_RES_PD 3  // weight prefetch distance (steps)
-#endif
 
 template <class S, int NG>
 struct ConvTResCfg {
@@ -33,7 +30,7 @@ struct ConvTResCfg {
   static constexpr int UNITS = NG * XROWS * 4;  // staging units (group, row, channel quad)
   static constexpr int UPT = (UNITS + 511) / 512;
   static constexpr int NS = NG * 2;            // MFMA steps (group, tap)
-  static constexpr int PD = CONVT_RES_PD;      // weight prefetch distance
+  static constexpr int PD = 3;                 // weight prefetch distance (2, 3, 5 measured equal)
   static_assert(LDSB <= 96 * 1024, "LDS window");
 };
 
@@ -182,13 +179,9 @@ void launch_res_s(const Conv1dArgs& a, int B, hipStream_t s) {
 }  // namespace
 
 // The x8 ConvTranspose layers with 128 or 256 input channels and a multiple of 256 rows, f16x3 /
-// bf16; TTS_MI355X_CONVT_RES=0 keeps conv1d_split_kernel (A/B runs)
+// bf16 (the others take conv1d_split_kernel)
 bool convT_res_supported(int mode, const Conv1dArgs& a) {
-  static const bool on = [] {
-    const char* e = std::getenv("TTS_MI355X_CONVT_RES");
-    return !(e && e[0] == '0');
-  }();
-  return on && (mode == MATH_FP32_F16X3 || mode == MATH_BF16) && a.ups == 8 && (a.Cin == 128 || a.Cin == 256) &&
+  return (mode == MATH_FP32_F16X3 || mode == MATH_BF16) && a.ups == 8 && (a.Cin == 128 || a.Cin == 256) &&
          a.Cout % 256 == 0 && a.Tout == a.Tin + 1 && a.pad == 1 && a.dil == 1 && a.zmode == 0 && !a.res && !a.mask;
 }
 

@@ -99,33 +99,14 @@ int conv1d_split_num_tiles(int mode) {
   return kNumSplitTiles;
 }
 
-namespace {
-int env_tile(const char* name) {  // a plain split tile index from the environment, else -1
-  const char* e = std::getenv(name);
-  const int t = e ? std::atoi(e) : -1;
-  return (t >= 0 && t < kNumSplitTiles && t != kSplitGateTile && t != kSplitWinoTile) ? t : -1;
-}
-}  // namespace
-
 // Tile choice per conv shape from the round-1 MI355X sweeps (profiles/r01_tune_conv_*.log).
 // Any tile is correct for any Cin: channels past Cin read 0.
 int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
   (void)res;
   if ((K - 1) * dil > (K - 1) * 5) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
   if (mode == MATH_FP32_F16X3) {
-    // TTS_MI355X_TILE_UPS64 / TTS_MI355X_TILE_UPSBIG=<idx> override the ConvTranspose tiles
-    // (K == 2, U*Cout rows <= 64 / > 64; A/B runs)
-    if (K == 2) {
-      static const int ups64 = env_tile("TTS_MI355X_TILE_UPS64"), upsbig = env_tile("TTS_MI355X_TILE_UPSBIG");
-      const int t = Cout <= 64 ? ups64 : upsbig;
-      if (t >= 0) return t;
-    }
-    // TTS_MI355X_TILE_BIG=<idx> overrides the tile of the Cout > 64 layers (A/B runs)
-    static const int big = [] {
-      const char* e = std::getenv("TTS_MI355X_TILE_BIG");
-      return e ? std::atoi(e) : 13;
-    }();
-    if (Cout > 64) return (big >= 0 && big < kNumSplitTiles) ? big : 13;
+    // ConvTranspose (K == 2) layers included: round-2 re-sweep, DESIGN.md section 4
+    if (Cout > 64) return 13;
     if (Cout > 32) return 10;
     return 14;  // one 16-channel group, 42 KB of LDS: 3 workgroups per CU
   }
@@ -146,26 +127,13 @@ void launch_conv1d_split(int mode, const Conv1dArgs& a, int B, int K, int tile, 
   // every addressed plane must stay below 2 GiB (32-bit buffer offsets, OOB marker bit 31)
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
-  // XCD-aware tile orders for multi-m-block launches (split_kernel.hpp), TTS_MI355X_XCD_REMAP:
-  //   1: an XCD's workgroups take one contiguous range with the m-block slowest (weights stay in
-  //      its L2; measured neutral: the weights re-read per XCD are served by the Infinity Cache)
-  //   2: the m-blocks of one column tile run together on one XCD (the input window is fetched
-  //      once per XCD instead of once per m-block)
-  static const int remap = [] {
-    const char* e = std::getenv("TTS_MI355X_XCD_REMAP");
-    return e ? std::atoi(e) : 0;
-  }();
   if (a.ups > 0 && convT_res_supported(mode, a)) {
     launch_convT_res(mode, a, B, s);
     return;
   }
-  Conv1dArgs ar = a;
-  const int gy = ceil_div(a.Cout, conv1d_split_tile(mode, tile).BM);
-  const int64_t nwg = (int64_t)ceil_div(a.Tout, conv1d_split_tile(mode, tile).BN) * gy * B;
-  ar.xcd_remap = gy > 1 && (remap == 1 || (remap == 2 && nwg % (8 * gy) == 0)) ? remap : 0;
-  if (mode == MATH_FP32_F16X3) launch_split_h3(ar, B, K, tile, s);
-  else if (mode == MATH_BF16) launch_split_b1(ar, B, K, tile, s);
-  else launch_split_x6(ar, B, K, tile, s);
+  if (mode == MATH_FP32_F16X3) launch_split_h3(a, B, K, tile, s);
+  else if (mode == MATH_BF16) launch_split_b1(a, B, K, tile, s);
+  else launch_split_x6(a, B, K, tile, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

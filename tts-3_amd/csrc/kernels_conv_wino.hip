@@ -26,21 +26,8 @@ void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
   TTS_REQUIRE((int64_t)a.Cin * a.Tin * 4 < (int64_t(1) << 31) && (int64_t)a.Cout * a.Tout * 4 < (int64_t(1) << 31), 3,
               "conv1d: a batch item's channel plane exceeds 2 GiB");
   // the 8-wave form needs 16-byte aligned input rows (every HiFiGAN MRF conv at >= 128 channels:
-  // T = 8 * (T_mel + 2 pad) and more); TTS_MI355X_WINO8=0 keeps the 4-wave form (A/B runs)
-  static const bool w8 = [] {
-    const char* e = std::getenv("TTS_MI355X_WINO8");
-    return !(e && e[0] == '0');
-  }();
-  // TTS_MI355X_WINO_XCD=1: the m-blocks of a column tile on one XCD (8-wave form, Cout > 128)
-  static const bool xcd = [] {
-    const char* e = std::getenv("TTS_MI355X_WINO_XCD");
-    return e && e[0] == '1';
-  }();
-  if (w8 && a.Tin % 4 == 0) {
-    Conv1dArgs ar = a;
-    ar.xcd_remap = xcd && a.Cout > 128 ? 2 : 0;  // wino8 launch_d checks the grid divisibility
-    wino8_detail::launch_s<SchemeH3>(ar, B, K, s);
-  }
+  // T = 8 * (T_mel + 2 pad) and more); other lengths take the 4-wave form
+  if (a.Tin % 4 == 0) wino8_detail::launch_s<SchemeH3>(a, B, K, s);
   else wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
   TTS_HIP_CHECK(hipGetLastError());
 }

@@ -20,9 +20,6 @@
 
 namespace tts {
 
-#ifndef PAIR_PIPE
-#define PAIR_PIPE 0  // build option: 1 = software-pipelined epilogue gathers at 64 channels (measured neutral)
-#endif
 
 // Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
 // 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 2 * LEAD output columns.
@@ -333,41 +330,22 @@ void resblock_pair_kernel(ResPairArgs pa) {
         for (int n = 0; n < TN; ++n) acc[m][n] *= sc2;
     }
     // C = 64: the software-pipelined epilogue (one memory latency per tile; registers allow it)
-    conv_epilogue<TM, TN, H3, C == 64 && PAIR_PIPE>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
+    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
   }
 }
 
 namespace {
-// TTS_MI355X_PAIR_ALLX=0 keeps the double-buffered per-group staging (A/B runs)
-bool pair_allx() {
-  static const bool v = [] {
-    const char* e = std::getenv("TTS_MI355X_PAIR_ALLX");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 template <class S, int K, int C, int GEO>
 void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
   // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32 (scripts/ab_pair_allx.sh)
-  if (C == 64 && pair_allx()) hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, true>), grid, dim3(256), 0, s, a);
+  if (C == 64) hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, false>), grid, dim3(256), 0, s, a);
-}
-
-// TTS_MI355X_PAIR_GEO64=0 selects the wide (256-column) geometry at 64 channels (A/B runs)
-int pair_geo64() {
-  static const int g = [] {
-    const char* e = std::getenv("TTS_MI355X_PAIR_GEO64");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return g;
 }
 
 template <class S, int K>
 void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
   if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
-  else if (C == 64 && pair_geo64() == 0) launch_pair_t<S, K, 64, 0>(a, B, s);
   else if (C == 64) launch_pair_t<S, K, 64, 1>(a, B, s);
   else throw Error(3, "resblock pair: channels must be 32 or 64");
 }
@@ -403,10 +381,6 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
   TTS_REQUIRE(a.c1.cvec == nullptr && a.c2.cvec == nullptr && a.c1.bias && a.c2.bias, 1,
               "resblock pair: biases required, no cond vector (both are staged in LDS)");
   TTS_REQUIRE((int64_t)C * a.c1.Tout * 4 < (int64_t(1) << 31), 3, "resblock pair: plane exceeds 2 GiB");
-  if (resblock_pp_enabled(mode, C, K)) {
-    launch_resblock_pp(mode, a, B, K, C, s);
-    return;
-  }
   if (mode == MATH_FP32_F16X3) launch_pair_s<SchemeH3>(a, B, K, C, s);
   else if (mode == MATH_BF16) launch_pair_s<SchemeB1>(a, B, K, C, s);
   else launch_pair_s<SchemeX6>(a, B, K, C, s);
@@ -790,28 +764,14 @@ void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
 }
 template <class S>
 void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
-  // C = 64: 128 columns (2 waves/SIMD, a quarter of the columns are halo) unless
-  // TTS_MI355X_RES3_GEO64=1 (192 columns, one wave per SIMD)
-  static const int geo64 = [] {
-    const char* e = std::getenv("TTS_MI355X_RES3_GEO64");
-    return (e && e[0] == '1') ? 1 : 2;
-  }();
-  // C = 128: 128 columns as 8 waves of 32 rows x 64 columns (two per SIMD) unless
-  // TTS_MI355X_RES3_GEO128=2 (2 x 2 waves of 64 x 64, one per SIMD); LDS 8 x 138 rows either way
-  static const int geo128 = [] {
-    const char* e = std::getenv("TTS_MI355X_RES3_GEO128");
-    return (e && e[0] == '2') ? 2 : 3;
-  }();
+  // C = 64: 128 columns (2 waves/SIMD, a quarter of the columns are halo; 192 columns at one
+  // wave per SIMD measured slower).  C = 128: 128 columns as 8 waves of 32 rows x 64 columns (two
+  // per SIMD; 2 x 2 waves of 64 x 64 measured slower); LDS 8 x 138 rows
   if (C == 32) launch_res3_t<S, 32, 0>(a, B, s);
   else if (C == 128) {
-    if constexpr (S::ROWB <= 80) {
-      if (geo128 == 2) launch_res3_t<S, 128, 2>(a, B, s);
-      else launch_res3_t<S, 128, 3>(a, B, s);
-    } else {
-      throw Error(3, "resblock3: 128 channels need a split scheme of at most 80-byte rows");
-    }
-  } else if (geo64 == 1) launch_res3_t<S, 64, 1>(a, B, s);
-  else launch_res3_t<S, 64, 2>(a, B, s);
+    if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 3>(a, B, s);
+    else throw Error(3, "resblock3: 128 channels need a split scheme of at most 80-byte rows");
+  } else launch_res3_t<S, 64, 2>(a, B, s);
 }
 }  // namespace
 

@@ -116,34 +116,7 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   const int half = lane >> 5;
   const int l32 = lane & 31;
 
-  // XCD-aware tile order (cdna_hip_programming.md T1, bijective form): blocks that share an XCD
-  // (same linear id mod 8) get one contiguous range of the (time tile, batch, m-block) order with
-  // the m-block slowest, so an XCD's L2 holds the weights of one or two m-blocks instead of all
-  // of them (the 8 / 16 m-block ConvTranspose layers stream 2-8 MB of weights per launch).
-  int bx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
-  if (a.xcd_remap == 2) {
-    // the m-blocks of one column tile run back to back on one XCD (consecutive workgroups of an
-    // XCD are linear ids 8 apart), so its L2 serves their shared input window once instead of
-    // each m-block fetching it again from the fabric (the x8 ConvTranspose layers have 8-16
-    // m-blocks per window).  The host sets it only when the grid is a multiple of 8 x gridDim.y.
-    const unsigned gx = gridDim.x, gy = gridDim.y;
-    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const unsigned q = orig >> 3;
-    mt = (int)(q % gy);
-    const unsigned c = (q / gy) * 8u + (orig & 7u);  // column tile (bx, b)
-    bx = (int)(c % gx);
-    b = (int)(c / gx);
-  } else if (a.xcd_remap) {
-    const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
-    const unsigned nwg = gx * gy * gz;
-    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const unsigned xcd = orig & 7u, q = nwg >> 3, r = nwg & 7u;
-    const unsigned wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-    bx = (int)(wgid % gx);
-    const unsigned rest = wgid / gx;
-    b = (int)(rest % gz);
-    mt = (int)(rest / gz);
-  }
+  const int bx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
   const int t0 = bx * BN;
   const int d = a.dil;
   const int XW = BN + (K - 1) * d;

@@ -98,19 +98,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const int grp = wave >> 2;  // 0: points 0-3 (+ no loads), 1: points 4-6 (+ the input DMA)
   const int half = lane >> 5;
   const int l32 = lane & 31;
-  int bx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
-  if (a.xcd_remap == 2) {
-    // the m-blocks of one column tile run back to back on one XCD (its workgroups are linear ids
-    // 8 apart), so they share the input window through that XCD's L2 instead of each fetching it
-    // (the host sets it only when the grid is a multiple of 8 x gridDim.y)
-    const unsigned gx = gridDim.x, gy = gridDim.y;
-    const unsigned orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const unsigned q = orig >> 3;
-    mt = (int)(q % gy);
-    const unsigned c = (q / gy) * 8u + (orig & 7u);
-    bx = (int)(c % gx);
-    b = (int)(c / gx);
-  }
+  const int bx = blockIdx.x, mt = blockIdx.y, b = blockIdx.z;
   const int t0 = bx * C::TW;
   const int Tin = a.Tin;
   const int Cin = a.Cin;
@@ -496,12 +484,6 @@ template <class S, int K, int D>
 void launch_d(const Conv1dArgs& a, int B, hipStream_t s) {
   using C = Wino8Cfg<S, K, D>;
   const dim3 grid(ceil_div(a.Tout, C::TW), ceil_div(a.Cout, 128), B);
-  if (a.xcd_remap == 2 && ((int64_t)grid.x * B) % 8 != 0) {
-    Conv1dArgs ar = a;  // the remap needs whole groups of 8 column tiles
-    ar.xcd_remap = 0;
-    launch_d<S, K, D>(ar, B, s);
-    return;
-  }
   if constexpr (D == 1) {
     if (a.in_slope == 1.f) {
       hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, false>), grid, dim3(512), 0, s, a);

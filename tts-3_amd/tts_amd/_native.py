@@ -28,6 +28,22 @@ TTS_ERR_OOM = 4
 # math modes (TTS_MATH_* in tts_mi355x.h)
 MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
+# the C-ABI revision these bindings were written for (tts_abi_version() in csrc/abi.cpp)
+ABI_VERSION = 111
+
+
+def default_math_mode(fp32_faithful_only: bool = True) -> str:
+    """Math mode of a module built without an explicit ``math_mode``: ``$TTS_MI355X_MATH_MODE`` if
+    set, else ``"f16x3"`` (fp32 in / fp32 out, measured at or below the exact-fp32 MFMA mode's error
+    against the fp64 oracle, DESIGN.md section 3, and 3x its speed).  ``bf16`` is a lower-precision
+    mode and is only taken from the environment when the caller allows it."""
+    m = os.environ.get("TTS_MI355X_MATH_MODE", "f16x3")
+    if m not in MATH_MODES:
+        raise ValueError(f"TTS_MI355X_MATH_MODE={m!r}: must be one of {sorted(MATH_MODES)}")
+    if fp32_faithful_only and m == "bf16":
+        raise ValueError("TTS_MI355X_MATH_MODE=bf16 is not fp32-faithful; pass math_mode='bf16' explicitly")
+    return m
+
 MAX_UPSAMPLES = 8
 MAX_KERNELS = 4
 MAX_DILATIONS = 4
@@ -252,12 +268,19 @@ def source_hash(pkg_dir: str = _PKG_DIR) -> str:
     return h.hexdigest()[:16]
 
 
+def build_info_fields(handle) -> dict:
+    """``tts_build_info()`` parsed: target=, src= (source hash) and defs= (build-option macros)."""
+    handle.tts_build_info.restype = c_char_p
+    handle.tts_build_info.argtypes = []
+    return dict(kv.split("=", 1) for kv in handle.tts_build_info().decode().split())
+
+
 def build_info() -> dict:
-    """Provenance of the loaded library: its stamped source hash and the file's own sha256."""
+    """Provenance of the loaded library: its stamped source hash, the build-option macros it was
+    compiled with, and the file's own sha256."""
     import hashlib
 
-    info = lib().tts_build_info().decode()
-    fields = dict(kv.split("=", 1) for kv in info.split())
+    fields = build_info_fields(lib())
     with open(LIB_PATH, "rb") as fh:
         fields["lib_sha256"] = hashlib.sha256(fh.read()).hexdigest()[:16]
     fields["lib_path"] = LIB_PATH
@@ -283,11 +306,30 @@ def lib() -> ctypes.CDLL:
             "(or __graft_entry__.build()); the MI355X path has no CPU fallback"
         )
     handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    handle.tts_abi_version.restype = c_int
+    handle.tts_abi_version.argtypes = []
+    abi = handle.tts_abi_version()
+    if abi != ABI_VERSION:
+        # argument lists differ between revisions: binding them to another revision passes
+        # pointers where the library expects sizes (garbage or a GPU fault), so refuse to load
+        raise RuntimeError(f"{LIB_PATH} implements C-ABI {abi}, these bindings need {ABI_VERSION}: "
+                           "rebuild it with `make -C tts-3_amd`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(handle, name)
         fn.restype = res
         fn.argtypes = args
     _lib = handle
+    stamp = build_info_fields(handle).get("src")
+    if stamp is not None and os.path.exists(os.path.join(_PKG_DIR, "Makefile")):
+        try:
+            want = source_hash()
+        except OSError:
+            want = None
+        if want is not None and stamp != want:
+            import warnings
+
+            warnings.warn(f"{LIB_PATH} was built from other sources (src={stamp}, tree={want}); "
+                          "rebuild it with `make -C tts-3_amd`", RuntimeWarning, stacklevel=2)
     return _lib
 
 

@@ -77,6 +77,9 @@ def scatter_batch(full: Optional[torch.Tensor], n: int, item_shape: Sequence[int
     if rank == src:
         if tuple(full.shape) != (n, *item_shape):
             raise ValueError(f"scatter_batch: full has shape {tuple(full.shape)}, expected {(n, *item_shape)}")
+        if full.dtype != buf.dtype or full.device != buf.device:
+            # the collective needs send and receive buffers of one dtype on the communicator's device
+            full = full.to(device=buf.device, dtype=buf.dtype)
         chunks = _equal_views(full, world)
         if chunks is None:
             chunks = []
@@ -108,8 +111,16 @@ def gather_batch(local: torch.Tensor, n: int, dst: int = 0, out: Optional[torch.
         dist.gather(buf, None, dst=dst)
         return None
     if even:
-        full = out if out is not None else torch.empty(n, *local.shape[1:], device=local.device, dtype=local.dtype)
+        # receive straight into `out` only when it is exactly the full tensor's layout; otherwise
+        # into a temporary (a bad `out` must not fail inside the collective after the peers have
+        # entered it: they would wait for the timeout), copied into `out` afterwards
+        direct = (out is not None and tuple(out.shape) == (n, *local.shape[1:]) and out.is_contiguous()
+                  and out.dtype == local.dtype and out.device == local.device)
+        full = out if direct else torch.empty(n, *local.shape[1:], device=local.device, dtype=local.dtype)
         dist.gather(buf, _equal_views(full, world), dst=dst)
+        if out is not None and not direct:
+            out.copy_(full)
+            return out
         return full
     outs = [torch.empty_like(buf) for _ in range(world)]
     dist.gather(buf, outs, dst=dst)

@@ -139,8 +139,10 @@ def _t(t: torch.Tensor) -> np.ndarray:
 class Decoder(nn.Module):
     def __init__(self, in_channels, hidden_channels, kernel_size, dilation_rate, num_flow_blocks,
                  num_coupling_layers, dropout_p=0.0, num_splits=4, num_squeeze=2, sigmoid_scale=False,
-                 c_in_channels=0, math_mode: str = "fp32"):
+                 c_in_channels=0, math_mode: Optional[str] = None):
         super().__init__()
+        if math_mode is None:
+            math_mode = N.default_math_mode()
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
         self.math_mode = math_mode

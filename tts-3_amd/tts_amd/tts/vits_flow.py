@@ -48,8 +48,10 @@ class ResidualCouplingBlock(nn.Module):
 
 class ResidualCouplingBlocks(nn.Module):
     def __init__(self, channels: int, hidden_channels: int, kernel_size: int, dilation_rate: int, num_layers: int,
-                 num_flows=4, cond_channels=0, math_mode: str = "fp32"):
+                 num_flows=4, cond_channels=0, math_mode: Optional[str] = None):
         super().__init__()
+        if math_mode is None:
+            math_mode = N.default_math_mode()
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
         self.math_mode = math_mode

@@ -36,7 +36,7 @@ class HifiDecoder(nn.Module):
         d_vector_dim=512,
         cond_d_vector_in_each_upsampling_layer=True,
         speaker_encoder_audio_config=None,
-        math_mode: str = "fp32",
+        math_mode: Optional[str] = None,
     ):
         super().__init__()
         self.input_sample_rate = input_sample_rate

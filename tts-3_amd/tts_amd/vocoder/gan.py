@@ -20,13 +20,20 @@ def _get(c: Any, key: str, default=None):
 
 def setup_generator(c: Any) -> HifiganGenerator:
     """``setup_generator`` (vocoder/models/__init__.py:34-41) for the HiFiGAN branch:
-    ``HifiganGenerator(in_channels=c.audio["num_mels"], out_channels=1, **c.generator_model_params)``."""
+    ``HifiganGenerator(in_channels=c.audio["num_mels"], out_channels=1, **c.generator_model_params)``.
+
+    The conv arithmetic comes from the config without code edits, first match wins:
+    ``generator_model_params["math_mode"]``, then a top-level ``math_mode`` field, then
+    ``$TTS_MI355X_MATH_MODE``, then ``"f16x3"`` (fp32-faithful, the measured bench mode).  A
+    reference config has neither field, so it gets f16x3."""
     name = str(_get(c, "generator_model", "hifigan_generator")).lower()
     if name not in "hifigan_generator":  # the reference's substring test (:40)
         raise NotImplementedError(f"generator {name!r}: only hifigan_generator runs on the MI355X path")
     audio = _get(c, "audio", {}) or {}
     num_mels = audio["num_mels"] if isinstance(audio, dict) else audio.num_mels
     params: Dict[str, Any] = dict(_get(c, "generator_model_params"))
+    if params.get("math_mode") is None:
+        params["math_mode"] = _get(c, "math_mode", None)
     return HifiganGenerator(in_channels=num_mels, out_channels=1, **params)
 
 

@@ -109,16 +109,26 @@ class HifiganGenerator(nn.Module):
         conv_pre_weight_norm: bool = True,
         conv_post_weight_norm: bool = True,
         conv_post_bias: bool = True,
-        math_mode: str = "fp32",
+        math_mode: Optional[str] = None,
         cond_in_each_up_layer: bool = False,
     ):
         """Arguments as the reference (:163-178).  ``math_mode`` selects how the conv contractions
-        run on MI355X: ``"fp32"`` (v_mfma_f32_32x32x2_f32) or ``"fp32x6"`` (fp32 operands split
-        exactly into 3 bf16 pieces, 6 cross products accumulated in fp32 on the bf16 matrix
-        cores; fp32-faithful, see include/tts_mi355x.h).  ``cond_in_each_up_layer`` is the XTTS
+        run on MI355X (all take and return fp32; include/tts_mi355x.h TTS_MATH_*):
+
+        * ``"f16x3"`` (the default, unless ``$TTS_MI355X_MATH_MODE`` names another): each fp32
+          operand scaled by an exact power of two and split into fp16 hi + lo, the three products
+          hi*hi + hi*lo + lo*hi accumulated in fp32 on the fp16 matrix cores.  Its error against the
+          fp64 oracle is at or below the exact-fp32 mode's at 3x the speed.
+        * ``"fp32"``: v_mfma_f32_32x32x2_f32, exact fp32 products.
+        * ``"fp32x6"``: 3 exact bf16 pieces per operand, the 6 leading cross products.
+        * ``"bf16"``: bf16 operands, fp32 accumulation (lower precision; VITS / Glow-TTS configs).
+
+        ``cond_in_each_up_layer`` is the XTTS
         generator's option (TTS/tts/layers/xtts/hifigan_decoder.py:199, :240-244, :276-279):
         ``o = ups[i](o) + conds[i](g)`` after every upsampling."""
         super().__init__()
+        if math_mode is None:
+            math_mode = N.default_math_mode()
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
         self.math_mode = math_mode
