@@ -11,7 +11,7 @@
  *       HifiganGenerator.remove_weight_norm :284-291 (weights arrive already folded)
  *   Glow-TTS decoder   TTS/tts/layers/glow_tts/decoder.py
  *       Decoder.__init__                 :68-111    -> tts_glow_decoder_create
- *       Decoder.forward(reverse=True)    :113-137   -> tts_glow_decoder_forward
+ *       Decoder.forward(reverse=True/False) :113-137 -> tts_glow_decoder_forward
  *       Decoder.store_inverse            :139-141   (W^-1 arrives precomputed)
  *   Glow-TTS encoder   TTS/tts/layers/glow_tts/encoder.py (rel_pos_transformer)
  *       Encoder.__init__                 :83-141    -> tts_glow_encoder_create
@@ -185,6 +185,7 @@ typedef struct TtsGlowDecoderCfg {
 /* Host weight order, per flow block b < num_flow_blocks (flows 3b, 3b+1, 3b+2):
  *   actnorm.logs [C2], actnorm.bias [C2]                          (C2 = in*num_squeeze)
  *   invconv.weight_inv [S][S]  (torch.inverse(weight), glow.py:139-141)
+ *   invconv.weight [S][S]      (the forward direction, glow.py:126-130; since ABI 112)
  *   coupling.start.weight [H][C2/2] (weight-norm folded), coupling.start.bias [H]
  *   if c_in_channels: wn.cond_layer.weight [2*H*L][c_in] (weight-norm folded), bias [2*H*L]
  *   for l < L: wn.in_layers.l.weight [2H][H][k], wn.in_layers.l.bias [2H]
@@ -195,16 +196,20 @@ int64_t tts_glow_decoder_weight_numel(const TtsGlowDecoderCfg* cfg, int idx);
 int tts_glow_decoder_create(const TtsGlowDecoderCfg* cfg, const float* const* host_weights,
                             int device, void** handle);
 int tts_glow_decoder_destroy(void* handle);
-/* y[B][C][T'] = Decoder.forward(x, x_mask, g, reverse=reverse)[0] with T' = T rounded down to a
- * multiple of num_squeeze (decoder.py:19); d_mask is [B][1][T] (0/1); d_g is the speaker vector
- * [B][c_in_channels] (the reference's g [B][c_in][1], decoder.py:113), NULL when c_in_channels == 0.
- * Only reverse = 1 is implemented (the inference direction, glow_tts.py:363). */
+/* (y, logdet) = Decoder.forward(x, x_mask, g, reverse=reverse) (decoder.py:113-137): y[B][C][T'] with
+ * T' = T rounded down to a multiple of num_squeeze (decoder.py:19); d_mask is [B][1][T] (0/1); d_g is
+ * the speaker vector [B][c_in_channels] (the reference's g [B][c_in][1]), NULL when c_in_channels == 0.
+ * reverse = 1: the inference direction (glow_tts.py:363), d_logdet unused (the reference returns None).
+ * reverse = 0: the flows in order (GlowTTS.decoder_inference, glow_tts.py:333); d_logdet [B] fp32
+ * receives logdet_tot (ActNorm + InvConvNear + coupling terms, summed per utterance in fp64 in a fixed
+ * order), or is NULL to skip it.  Since ABI 112 (d_logdet added). */
 int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
-                             int C, int T, int reverse, float* d_y, void* hip_stream);
+                             int C, int T, int reverse, float* d_y, float* d_logdet, void* hip_stream);
 /* Same with a hipEvent pair around every launch (synchronises; see tts_hifigan_forward_profiled). */
 int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
-                                      int B, int C, int T, int reverse, float* d_y, void* hip_stream,
-                                      TtsLaunchRecord* records, int max_records, int* n_records);
+                                      int B, int C, int T, int reverse, float* d_y, float* d_logdet,
+                                      void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                      int* n_records);
 
 /* ------------------------------------------------------------------------------------ */
 /* Glow-TTS encoder (rel_pos_transformer) and the GlowTTS.inference glue                   */
@@ -345,14 +350,55 @@ int64_t tts_vits_flow_weight_numel(const TtsVitsFlowCfg* cfg, int index);
 int tts_vits_flow_create(const TtsVitsFlowCfg* cfg, const float* const* host_weights, int device,
                          void** handle);
 int tts_vits_flow_destroy(void* handle);
-/* y[B][C][T] = ResidualCouplingBlocks(x, mask, g, reverse=True).  x, y: [B][C][T] fp32 (y may
- * equal x: in place), mask: [B][T], g: [B][cond_channels] (NULL when cond_channels == 0).
- * reverse must be 1. */
+/* y[B][C][T] = ResidualCouplingBlocks(x, mask, g, reverse=reverse) (networks.py:217-232).  x, y:
+ * [B][C][T] fp32 (y may equal x: in place), mask: [B][T], g: [B][cond_channels] (NULL when
+ * cond_channels == 0).  reverse = 1: the inference direction (vits.py:1155); reverse = 0: the
+ * posterior side of voice conversion, z_p = flow(z, y_mask, g) (vits.py:1226; since ABI 112). */
 int tts_vits_flow_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
                           int C, int T, int reverse, float* d_y, void* hip_stream);
 int tts_vits_flow_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
                                    int B, int C, int T, int reverse, float* d_y, void* hip_stream,
                                    TtsLaunchRecord* records, int max_records, int* n_records);
+
+/* ------------------------------------------------------------------------------------ */
+/* VITS posterior encoder (TTS/tts/layers/vits/networks.py:235-288), since ABI 112        */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors PosteriorEncoder.__init__ (networks.py:236-273); VITS builds it from the linear
+ * spectrogram (vits.py:594-602: in = fft_size/2 + 1 = 513, out = hidden = 192, k5, d1, 16 layers). */
+typedef struct TtsVitsPosteriorCfg {
+  int in_channels;     /* 513 */
+  int out_channels;    /* 192 */
+  int hidden_channels; /* 192 */
+  int kernel_size;     /* 5 */
+  int dilation_rate;   /* 1 */
+  int num_layers;      /* 16 */
+  int cond_channels;   /* speaker embedding size, 0 = none */
+  int math_mode;       /* TTS_MATH_* (f16x3 / fp32x6 / fp32 / bf16) */
+} TtsVitsPosteriorCfg;
+
+/* Host weight order (weight norm folded):
+ *   pre.weight [H][in], pre.bias [H]
+ *   for l < L: enc.in_layers.l.weight [2H][H][k], bias [2H]
+ *   for l < L: enc.res_skip_layers.l.weight [l<L-1 ? 2H : H][H], bias
+ *   if cond_channels: enc.cond_layer.weight [2*H*L][cond_channels], bias [2*H*L]
+ *   proj.weight [2*out][H], proj.bias [2*out] */
+int tts_vits_posterior_num_weights(const TtsVitsPosteriorCfg* cfg);
+int64_t tts_vits_posterior_weight_numel(const TtsVitsPosteriorCfg* cfg, int index);
+int tts_vits_posterior_create(const TtsVitsPosteriorCfg* cfg, const float* const* host_weights, int device,
+                              void** handle);
+int tts_vits_posterior_destroy(void* handle);
+/* (z, m, logs) = PosteriorEncoder.forward(x, x_lengths, g)[:3] (networks.py:275-288): x [B][in][T],
+ * mask [B][T] (sequence_mask(x_lengths)), g [B][cond_channels] or NULL, eps [B][out][T] the standard
+ * normal sample the reference draws with torch.randn_like (NULL: zero noise, z = m); z, m, logs
+ * [B][out][T] fp32 (m or logs may be NULL when not wanted). */
+int tts_vits_posterior_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                               const float* d_eps, int B, int C, int T, float* d_z, float* d_m, float* d_logs,
+                               void* hip_stream);
+int tts_vits_posterior_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                                        const float* d_eps, int B, int C, int T, float* d_z, float* d_m,
+                                        float* d_logs, void* hip_stream, TtsLaunchRecord* records,
+                                        int max_records, int* n_records);
 
 /* ------------------------------------------------------------------------------------ */
 /* Single-op entry points (test / tuning surface).  These pack the host weights into a     */

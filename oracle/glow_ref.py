@@ -124,3 +124,68 @@ def glow_decoder_reverse(
     if num_squeeze > 1:
         x, x_mask = unsqueeze(x, x_mask, num_squeeze)
     return x
+
+
+def glow_decoder_forward(
+    sd: Dict[str, torch.Tensor],
+    x: torch.Tensor,
+    x_mask: torch.Tensor,
+    in_channels: int = 80,
+    hidden_channels: int = 192,
+    kernel_size: int = 5,
+    dilation_rate: int = 1,
+    num_flow_blocks: int = 12,
+    num_coupling_layers: int = 4,
+    num_splits: int = 4,
+    num_squeeze: int = 2,
+    sigmoid_scale: bool = False,
+    dtype=torch.float64,
+    fold_dtype=torch.float32,
+    g: torch.Tensor = None,
+    **_unused,
+):
+    """Decoder.forward(x, x_mask, g, reverse=False) -> (z, logdet [B]) (decoder.py:119-133):
+    squeeze, then per block in order ActNorm (normalization.py:99-101: z = (bias + exp(logs) * x) *
+    mask, logdet = sum(logs) * x_len), InvConvNear (glow.py:126-135: conv2d with W itself,
+    logdet = logdet(W) * (C / S) * x_len), CouplingBlock (glow.py:225-227: z1 = (t + exp(s) * x1) *
+    mask, logdet = sum(s * mask)); unsqueeze."""
+    w = fold_weight_norm({k: v for k, v in sd.items() if ".start." not in k}, dtype, fold_dtype)
+    w.update(fold_weight_norm({k: v for k, v in sd.items() if ".start." in k}, dtype, dtype))
+    x = x.to(dtype)
+    x_mask = x_mask.to(dtype)
+    if g is not None:
+        g = g.to(dtype)
+    if num_squeeze > 1:
+        x, x_mask = squeeze(x, x_mask, num_squeeze)
+    C2 = x.size(1)
+    S = num_splits
+    H = hidden_channels
+    x_len = torch.sum(x_mask, [1, 2])
+    logdet = torch.zeros(x.size(0), dtype=dtype)
+    for f in range(num_flow_blocks):
+        a, c, cb = 3 * f, 3 * f + 1, 3 * f + 2
+        # ActNorm forward
+        x = (w[f"flows.{a}.bias"] + torch.exp(w[f"flows.{a}.logs"]) * x) * x_mask
+        logdet = logdet + torch.sum(w[f"flows.{a}.logs"]) * x_len
+        # InvConvNear forward
+        b, cc, tt = x.size()
+        wf = w[f"flows.{c}.weight"]
+        xg = x.view(b, 2, cc // S, S // 2, tt).permute(0, 1, 3, 2, 4).contiguous().view(b, S, cc // S, tt)
+        z = F.conv2d(xg, wf.view(S, S, 1, 1))
+        x = z.view(b, 2, S // 2, cc // S, tt).permute(0, 1, 3, 2, 4).contiguous().view(b, cc, tt) * x_mask
+        logdet = logdet + torch.logdet(wf) * (cc / S) * x_len
+        # CouplingBlock forward
+        pre = f"flows.{cb}"
+        x0, x1 = x[:, : C2 // 2], x[:, C2 // 2 :]
+        h = F.conv1d(x0, w[f"{pre}.start.weight"], w[f"{pre}.start.bias"]) * x_mask
+        h = _wn(w, h, x_mask, num_coupling_layers, H, kernel_size, dilation_rate, pre, g)
+        out = F.conv1d(h, w[f"{pre}.end.weight"], w[f"{pre}.end.bias"])
+        t, s = out[:, : C2 // 2], out[:, C2 // 2 :]
+        if sigmoid_scale:
+            s = torch.log(1e-6 + torch.sigmoid(s + 2))
+        z1 = (t + torch.exp(s) * x1) * x_mask
+        logdet = logdet + torch.sum(s * x_mask, [1, 2])
+        x = torch.cat([x0, z1], 1)
+    if num_squeeze > 1:
+        x, x_mask = unsqueeze(x, x_mask, num_squeeze)
+    return x, logdet

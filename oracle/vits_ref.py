@@ -1,13 +1,15 @@
 """ORACLE — test infrastructure only.  Never imported by the product path (tts-3_amd/).
 
-CPU restatement of the VITS flow in the reverse (inference) direction in ``torch.nn.functional``,
-fp32 or fp64.  Follows Coqui TTS 0.22.0:
+CPU restatement of the VITS flow (both directions) and the posterior encoder in
+``torch.nn.functional``, fp32 or fp64.  Follows Coqui TTS 0.22.0:
 
 * ``TTS/tts/layers/vits/networks.py:217-232``  ResidualCouplingBlocks.forward(reverse=True):
   for flow in reversed(flows): x = flip(x, [1]); x = flow(x, mask, g, reverse=True)
 * ``:144-166``  ResidualCouplingBlock.forward (mean_only=True, the VITS setting :213):
   x0, x1 = split halves; h = pre(x0) * mask; h = WN(h, mask, g); m = post(h) * mask;
   x1 = (x1 - m) * exp(-0) * mask; cat(x0, x1)
+* ``:225-228``  forward(reverse=False): for flow in flows: x = flow(x); x = flip(x, [1])
+* ``:235-288``  PosteriorEncoder: pre -> WN -> proj -> split -> (m + eps * exp(logs)) * mask
 * ``TTS/tts/layers/generic/wavenet.py:94-115``  WN with the optional cond_layer (:98-99,
   g_l = cond[:, 2H*i : 2H*(i+1)], :103-107) and the fused gate (:6-13)
 
@@ -75,3 +77,64 @@ def vits_flow_reverse(
         x1 = (x1 - m) * torch.exp(-torch.zeros_like(m)) * x_mask
         x = torch.cat([x0, x1], 1)
     return x
+
+
+def vits_flow_forward(
+    sd: Dict[str, torch.Tensor],
+    x: torch.Tensor,
+    x_mask: torch.Tensor,
+    g: Optional[torch.Tensor] = None,
+    channels: int = 192,
+    hidden_channels: int = 192,
+    kernel_size: int = 5,
+    dilation_rate: int = 1,
+    num_layers: int = 4,
+    num_flows: int = 4,
+    dtype=torch.float64,
+    **_unused,
+):
+    """ResidualCouplingBlocks.forward(reverse=False) (networks.py:225-228): for flow in flows:
+    x = flow(x) (:154-160: x1 = m + x1 * exp(0) * mask); x = flip(x, [1])."""
+    w = fold_weight_norm(sd, dtype, dtype)
+    x = x.to(dtype)
+    x_mask = x_mask.to(dtype)
+    g = g.to(dtype) if g is not None else None
+    half = channels // 2
+    for f in range(num_flows):
+        pre = f"flows.{f}"
+        x0, x1 = x[:, :half], x[:, half:]
+        h = F.conv1d(x0, w[f"{pre}.pre.weight"], w[f"{pre}.pre.bias"]) * x_mask
+        h = _wn(w, h, x_mask, g, f"{pre}.enc", num_layers, hidden_channels, kernel_size, dilation_rate)
+        m = F.conv1d(h, w[f"{pre}.post.weight"], w[f"{pre}.post.bias"]) * x_mask
+        x1 = m + x1 * torch.exp(torch.zeros_like(m)) * x_mask
+        x = torch.flip(torch.cat([x0, x1], 1), [1])
+    return x
+
+
+def vits_posterior(
+    sd: Dict[str, torch.Tensor],
+    x: torch.Tensor,
+    x_mask: torch.Tensor,
+    eps: Optional[torch.Tensor] = None,
+    g: Optional[torch.Tensor] = None,
+    num_layers: int = 16,
+    hidden_channels: int = 192,
+    out_channels: int = 192,
+    kernel_size: int = 5,
+    dilation_rate: int = 1,
+    dtype=torch.float64,
+    **_unused,
+):
+    """PosteriorEncoder.forward (networks.py:275-288) with the noise given: h = pre(x) * mask;
+    h = WN(h, mask, g); stats = proj(h) * mask; m, logs = split; z = (m + eps * exp(logs)) * mask.
+    Returns (z, m, logs)."""
+    w = fold_weight_norm(sd, dtype, dtype)
+    x = x.to(dtype)
+    x_mask = x_mask.to(dtype)
+    g = g.to(dtype) if g is not None else None
+    h = F.conv1d(x, w["pre.weight"], w["pre.bias"]) * x_mask
+    h = _wn(w, h, x_mask, g, "enc", num_layers, hidden_channels, kernel_size, dilation_rate)
+    stats = F.conv1d(h, w["proj.weight"], w["proj.bias"]) * x_mask
+    m, logs = torch.split(stats, out_channels, dim=1)
+    e = eps.to(dtype) if eps is not None else torch.zeros_like(m)
+    return (m + e * torch.exp(logs)) * x_mask, m, logs

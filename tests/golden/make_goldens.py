@@ -60,6 +60,13 @@ def import_reference_vits_flow():
     return ResidualCouplingBlocks
 
 
+def import_reference_vits_posterior():
+    import_reference()
+    from TTS.tts.layers.vits.networks import PosteriorEncoder
+
+    return PosteriorEncoder
+
+
 def import_reference_glow_tts():
     import_reference()
     from TTS.tts.layers.glow_tts.decoder import Decoder
@@ -286,7 +293,55 @@ def vits_flow_case(ResidualCouplingBlocks, name, cfg, seed, B, T, lengths, x_see
           f"max|fp32-fp64| {np.abs(y32.numpy() - y64.numpy()).max():.2e}")
 
 
+def vits_posterior_case(PosteriorEncoder, name, cfg, seed, B, T, lengths, x_seed):
+    """G13: VITS PosteriorEncoder (networks.py:235-288).  The reference draws its noise with
+    torch.randn_like(mean) (:287): the fp32 run draws it from a fixed seed, the same draw is stored
+    as ``eps``, and the fp64 z is formed from the fp64 mean / log_scale with that eps."""
+    torch.manual_seed(0)
+    ref = PosteriorEncoder(cfg["in_channels"], cfg["out_channels"], cfg["hidden_channels"], cfg["kernel_size"],
+                           cfg["dilation_rate"], cfg["num_layers"], cond_channels=cfg["cond_channels"])
+    sd = synthetic.vits_posterior_state_dict(**cfg, seed=seed)
+    ref.load_state_dict(sd)
+    ref.eval()
+    gen = torch.Generator().manual_seed(x_seed)
+    x = torch.randn(B, cfg["in_channels"], T, generator=gen)
+    g = torch.randn(B, cfg["cond_channels"], 1, generator=gen) if cfg["cond_channels"] else None
+    lengths_t = torch.tensor(lengths)
+    with torch.no_grad():
+        torch.manual_seed(777)
+        z32, m32, ls32, mask = ref(x, lengths_t, g=g)
+        torch.manual_seed(777)
+        eps = torch.randn(B, cfg["out_channels"], T)  # the draw randn_like(mean) made
+        assert torch.equal(z32, (m32 + eps * torch.exp(ls32)) * mask)
+        ref64 = ref.double()
+        _, m64, ls64, mask64 = ref64(x.double(), lengths_t, g=g.double() if g is not None else None)
+        z64 = (m64 + eps.double() * torch.exp(ls64)) * mask64
+    meta = dict(kind="vits_posterior", config=cfg, seed=seed, x_seed=x_seed, B=B, T=T, lengths=lengths)
+    arrays = dict(x=x.numpy(), lengths=np.array(lengths), eps=eps.numpy(), mask=mask.numpy(), z_ref_fp32=z32.numpy(),
+                  m_ref_fp64=m64.numpy(), logs_ref_fp64=ls64.numpy(), z_ref_fp64=z64.numpy())
+    if g is not None:
+        arrays["g"] = g.numpy()
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: z {tuple(z32.shape)} std {z32.std():.4f} "
+          f"max|fp32-fp64| {np.abs(z32.numpy() - z64.numpy()).max():.2e}")
+
+
+def main_vits_posterior():
+    PosteriorEncoder = import_reference_vits_posterior()
+    from tts_amd.config import VITS_POSTERIOR
+
+    vits_posterior_case(PosteriorEncoder, "vits_posterior_b2_t37", dict(VITS_POSTERIOR, cond_channels=0), seed=1357,
+                        B=2, T=37, lengths=[37, 20], x_seed=51)
+    small = dict(in_channels=40, out_channels=16, hidden_channels=32, kernel_size=5, dilation_rate=2, num_layers=3,
+                 cond_channels=8)
+    vits_posterior_case(PosteriorEncoder, "vits_posterior_cond_b3_t29", small, seed=1358, B=3, T=29,
+                        lengths=[29, 13, 1], x_seed=52)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "vits_posterior":
+        return main_vits_posterior()
     if len(sys.argv) > 1 and sys.argv[1] == "vits":
         return main_vits()
     if len(sys.argv) > 1 and sys.argv[1] == "glow_tts":

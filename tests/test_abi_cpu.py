@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == N.ABI_VERSION == 111
+    assert N.lib().tts_abi_version() == N.ABI_VERSION == 112
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -194,7 +194,7 @@ def test_glow_decoder_surface():
     d.store_inverse()
     ws = d._weight_list()
     n = N.lib().tts_glow_decoder_num_weights(ctypes.byref(d._cfg))
-    assert n == len(ws) == 12 * (5 + 4 * 4 + 2)
+    assert n == len(ws) == 12 * (6 + 4 * 4 + 2)  # invconv weight_inv and weight (ABI 112)
     for i, w in enumerate(ws):
         assert N.lib().tts_glow_decoder_weight_numel(ctypes.byref(d._cfg), i) == w.size
     # W^-1 identical to the oracle's (reference store_inverse semantics)
@@ -203,7 +203,7 @@ def test_glow_decoder_surface():
     assert torch.equal(winv, torch.inverse(wf.t().contiguous().t()))
     with pytest.raises(RuntimeError, match="ROCm device"):
         d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), reverse=True)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="ROCm device"):
         d(torch.zeros(1, 80, 8), torch.ones(1, 1, 8), reverse=False)
 
 
@@ -219,7 +219,7 @@ def test_glow_decoder_speaker_surface():
     d.store_inverse()
     ws = d._weight_list()
     n = N.lib().tts_glow_decoder_num_weights(ctypes.byref(d._cfg))
-    assert n == len(ws) == 3 * 25
+    assert n == len(ws) == 3 * 26
     for i, w in enumerate(ws):
         assert N.lib().tts_glow_decoder_weight_numel(ctypes.byref(d._cfg), i) == w.size
     with pytest.raises(RuntimeError, match="ROCm device"):
@@ -231,11 +231,11 @@ def test_glow_config_validation():
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
     assert b"num_splits" in N.lib().tts_last_error()
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 16)  # speaker-conditioned: + cond_layer w, b per flow
-    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 25
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 26
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, -1)
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, N.MATH_MODES["f16x3"])
-    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 23  # f16x3 accepted (23 tensors per flow)
+    assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == 12 * 24  # f16x3 accepted (24 tensors per flow)
     c = N.TtsGlowDecoderCfg(80, 192, 5, 1, 12, 4, 4, 2, 0, 0, 9)
     assert N.lib().tts_glow_decoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
 

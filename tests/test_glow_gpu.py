@@ -149,3 +149,59 @@ def test_glow_speaker_gate_fusion_bitwise(cuda_device, mode, monkeypatch):
         monkeypatch.setenv("TTS_MI355X_FLOW_GATE", fused)
         outs.append(build(cfg, 29, cuda_device, mode)(x, m, g=g, reverse=True)[0])
     assert torch.equal(outs[0], outs[1])
+
+
+# ----------------------------------------------------------------------------- forward direction
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
+def test_glow_forward_vs_reference(cuda_device, name, meta, arr, mode):
+    """reverse=False (GlowTTS.decoder_inference's first pass, glow_tts.py:333): the reference's own
+    forward output on its fp64 reverse output (the fixture's roundtrip_fp64 / logdet_fp64)."""
+    d = build(meta["config"], meta["seed"], cuda_device, mode)
+    y = torch.from_numpy(arr["out_ref_fp64"]).float()
+    m = torch.from_numpy(arr["mask"])[:, :, : y.shape[2]]
+    g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
+    z, logdet = d(y.to(cuda_device), m.to(cuda_device), g=g, reverse=False)
+    assert z.shape == arr["roundtrip_fp64"].shape and logdet.shape == (y.shape[0],)
+    ref_ld = arr["logdet_fp64"]
+    if mode == "bf16":
+        assert_close_fp32(z.cpu(), arr["roundtrip_fp64"], f"{name} forward", BF16_MAX_ABS, BF16_REL_RMS)
+        assert np.abs(logdet.cpu().numpy() - ref_ld).max() <= 3e-2 * max(1.0, np.abs(ref_ld).max())
+    else:
+        assert_close_fp32(z.cpu(), arr["roundtrip_fp64"], f"{name} forward", GLOW_MAX_ABS, GLOW_REL_RMS)
+        # logdet sums ~1e3 terms per utterance: 1e-5 relative of its magnitude
+        assert np.abs(logdet.cpu().numpy() - ref_ld).max() <= 1e-5 * max(1.0, np.abs(ref_ld).max()), (logdet, ref_ld)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
+@pytest.mark.parametrize("B,T,lengths", [(1, 2, [2]), (3, 65, [65, 30, 1]), (2, 400, [400, 223])])
+def test_glow_forward_vs_oracle_and_roundtrip(cuda_device, B, T, lengths, mode):
+    """Forward against the fp64 oracle (z and logdet) on ragged masks, and forward o reverse = id
+    on the kept frames (decoder.py:25: frame pair (2t, 2t+1) survives iff mask[2t+1])."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    d = build(cfg, 98, cuda_device, mode)
+    gen = torch.Generator().manual_seed(T + 1)
+    x = torch.randn(B, 80, T, generator=gen)
+    m = (torch.arange(T)[None] < torch.tensor(lengths)[:, None]).float().unsqueeze(1)
+    z, logdet = d(x.to(cuda_device), m.to(cuda_device), reverse=False)
+    zr, ldr = glow_ref.glow_decoder_forward(synthetic.glow_decoder_state_dict(**cfg, seed=98), x, m, **cfg)
+    assert_close_fp32(z.cpu(), zr, f"glow forward B={B} T={T}", GLOW_MAX_ABS, GLOW_REL_RMS)
+    assert np.abs(logdet.cpu().double().numpy() - ldr.numpy()).max() <= 1e-5 * max(1.0, ldr.abs().max().item())
+    T2 = z.shape[2]
+    y, _ = d(z, m[:, :, :T2].to(cuda_device), reverse=True)
+    keep = m[:, :, 1:T2:2].repeat_interleave(2, dim=2)
+    assert max_abs((y.cpu() * keep).numpy(), (x[:, :, :T2] * keep).numpy()) < 1e-4
+
+
+def test_glow_forward_deterministic_and_batch_invariant(cuda_device):
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=12,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    d = build(cfg, 97, cuda_device, "f16x3")
+    x = torch.randn(4, 80, 301, generator=torch.Generator().manual_seed(4)).to(cuda_device)
+    m = torch.ones(4, 1, 301, device=cuda_device)
+    z, ld = d(x, m, reverse=False)
+    z2, ld2 = d(x, m, reverse=False)
+    assert torch.equal(z, z2) and torch.equal(ld, ld2)
+    z1, ld1 = d(x[2:3], m[2:3], reverse=False)
+    assert torch.equal(z1[0], z[2]) and torch.equal(ld1[0], ld[2])

@@ -219,3 +219,28 @@ def test_multispeaker_speaker_ids_vs_oracle(cuda_device):
         m.inference(tok, {"x_lengths": lens})
     with pytest.raises(ValueError):
         m.inference(tok, {"x_lengths": lens, "speaker_ids": sid, "d_vectors": torch.zeros(3, H)})
+
+
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
+def test_decoder_inference_vs_oracle(cuda_device, mode):
+    """GlowTTS.decoder_inference (glow_tts.py:319-339): decoder forward (mel -> z) then reverse, on
+    device, against the fp64 oracle chain; the forward-reverse pair returns the mel on the frames
+    the squeeze keeps."""
+    name, meta, arr = goldens("glow_tts")[0]
+    m = build_glow_tts(meta, cuda_device, decoder_math_mode=mode)
+    gen = torch.Generator().manual_seed(13)
+    B, T = 3, 91
+    y = torch.randn(B, T, 80, generator=gen)
+    lengths = torch.tensor([91, 60, 2])
+    out = m.decoder_inference(y.to(cuda_device), lengths.to(cuda_device))
+    assert out["logdet"] is None
+    yo = out["model_outputs"].cpu()
+    T2 = yo.shape[1]
+    dcfg = meta["decoder"]
+    sd = synthetic.glow_decoder_state_dict(**dcfg, seed=meta["dseed"])
+    mask = (torch.arange(T)[None] < lengths[:, None]).float().unsqueeze(1)
+    z, _ = glow_ref.glow_decoder_forward(sd, y.transpose(1, 2), mask, **dcfg)
+    ref = glow_ref.glow_decoder_reverse(sd, z, mask[:, :, :T2], **dcfg)
+    assert_close_fp32(yo.transpose(1, 2), ref, f"decoder_inference ({mode})", MEL_MAX_ABS, MEL_REL_RMS)
+    keep = mask[:, :, 1:T2:2].repeat_interleave(2, dim=2)
+    assert max_abs((yo.transpose(1, 2) * keep).numpy(), (y.transpose(1, 2)[:, :, :T2] * keep).numpy()) < 1e-4

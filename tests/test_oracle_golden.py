@@ -83,6 +83,21 @@ def test_glow_reference_roundtrip_fixture(name, meta, arr):
     assert max_abs(arr["roundtrip_fp64"] * m, x) < 1e-4
 
 
+@pytest.mark.parametrize("name,meta,arr", GLOW, ids=[g[0] for g in GLOW])
+def test_glow_forward_oracle_matches_reference(name, meta, arr):
+    """The forward direction (reverse=False) against the reference's own forward pass, which the
+    fixture ran on its fp64 reverse output (make_goldens.py glow_case): z and logdet."""
+    cfg = meta["config"]
+    sd = synthetic.glow_decoder_state_dict(**cfg, seed=meta["seed"])
+    g = torch.from_numpy(arr["g"]) if "g" in arr else None
+    y = torch.from_numpy(arr["out_ref_fp64"])
+    m = torch.from_numpy(arr["mask"])[:, :, : y.shape[2]]
+    z, logdet = glow_ref.glow_decoder_forward(sd, y, m, dtype=torch.float64, g=g, **cfg)
+    assert z.shape == arr["roundtrip_fp64"].shape
+    assert max_abs(z.numpy(), arr["roundtrip_fp64"]) < 1e-10
+    assert np.abs(logdet.numpy() - arr["logdet_fp64"]).max() < 1e-8 * max(1.0, np.abs(arr["logdet_fp64"]).max())
+
+
 VITS = goldens("vits_flow")
 
 
@@ -106,6 +121,33 @@ def test_vits_flow_reference_roundtrip_fixture(name, meta, arr):
     m = arr["mask"]
     assert max_abs(arr["roundtrip_fp64"] * m, arr["x"] * m) < 1e-9
     assert len(VITS) == 2
+
+
+@pytest.mark.parametrize("name,meta,arr", VITS, ids=[g[0] for g in VITS])
+def test_vits_flow_forward_oracle_matches_reference(name, meta, arr):
+    cfg = meta["config"]
+    sd = synthetic.vits_flow_state_dict(**cfg, seed=meta["seed"])
+    g = torch.from_numpy(arr["g"]) if "g" in arr else None
+    z = vits_ref.vits_flow_forward(sd, torch.from_numpy(arr["out_ref_fp64"]), torch.from_numpy(arr["mask"]), g,
+                                   dtype=torch.float64, **cfg)
+    assert max_abs(z.numpy(), arr["roundtrip_fp64"]) < 1e-10
+
+
+POSTERIOR = goldens("vits_posterior")
+
+
+@pytest.mark.parametrize("name,meta,arr", POSTERIOR, ids=[g[0] for g in POSTERIOR])
+def test_vits_posterior_oracle_matches_reference(name, meta, arr):
+    cfg = meta["config"]
+    sd = synthetic.vits_posterior_state_dict(**cfg, seed=meta["seed"])
+    g = torch.from_numpy(arr["g"]) if "g" in arr else None
+    x, m, eps = torch.from_numpy(arr["x"]), torch.from_numpy(arr["mask"]), torch.from_numpy(arr["eps"])
+    z, mean, logs = vits_ref.vits_posterior(sd, x, m, eps, g, dtype=torch.float64, **cfg)
+    assert max_abs(z.numpy(), arr["z_ref_fp64"]) < 1e-10
+    assert max_abs(mean.numpy(), arr["m_ref_fp64"]) < 1e-10 and max_abs(logs.numpy(), arr["logs_ref_fp64"]) < 1e-10
+    z32, _, _ = vits_ref.vits_posterior(sd, x, m, eps, g, dtype=torch.float32, **cfg)
+    assert max_abs(z32.numpy(), arr["z_ref_fp32"]) < 1e-5
+    assert len(POSTERIOR) == 2
 
 
 def test_synthetic_weights_deterministic():

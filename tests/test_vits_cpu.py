@@ -57,5 +57,30 @@ def test_cpu_module_refuses_to_run():
     f = _flow()
     with pytest.raises(RuntimeError, match="ROCm device"):
         f(torch.zeros(1, 192, 8), torch.ones(1, 1, 8), reverse=True)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="ROCm device"):
         f(torch.zeros(1, 192, 8), torch.ones(1, 1, 8), reverse=False)
+
+
+def test_posterior_encoder_surface():
+    lib = N.lib()
+    """PosteriorEncoder: the reference key set (networks.py:269-273, WN weight-normed) loads strictly,
+    the weight inventory lines up with the C-ABI's, and the module refuses to run off-device."""
+    from tts_amd import synthetic
+    from tts_amd.tts import PosteriorEncoder
+
+    for cond in (0, 8):
+        pe = PosteriorEncoder(513, 192, 192, 5, 1, 16, cond_channels=cond)
+        sd = synthetic.vits_posterior_state_dict(cond_channels=cond, seed=3)
+        pe.load_state_dict(sd)  # strict
+        assert list(pe.state_dict().keys()) == list(sd.keys())
+        ws = pe._weight_list()
+        n = lib.tts_vits_posterior_num_weights(ctypes.byref(pe._cfg))
+        assert n == len(ws) == 2 + 4 * 16 + (2 if cond else 0) + 2
+        for i, w in enumerate(ws):
+            assert lib.tts_vits_posterior_weight_numel(ctypes.byref(pe._cfg), i) == w.size
+        with pytest.raises(RuntimeError, match="ROCm device"):
+            pe(torch.zeros(1, 513, 8), torch.tensor([8]))
+    c = N.TtsVitsPosteriorCfg(513, 192, 192, 4, 1, 16, 0, 2)
+    assert lib.tts_vits_posterior_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    assert lib.tts_vits_posterior_create(None, None, 0, None) == N.TTS_ERR_INVALID
+    assert lib.tts_vits_posterior_destroy(None) == N.TTS_OK

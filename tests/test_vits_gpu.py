@@ -125,3 +125,99 @@ def test_vits_x0_statistics_match_prepass(cuda_device, cond, monkeypatch):
         f, _ = build(cfg, 37, cuda_device, "f16x3")
         outs.append(f(x, mask, g=g, reverse=True))
     assert torch.equal(outs[0], outs[1])
+
+
+# ----------------------------------------------------------------------------- forward direction
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name,meta,arr", VITS, ids=[g[0] for g in VITS])
+def test_vits_flow_forward_vs_reference(cuda_device, name, meta, arr, mode):
+    """reverse=False (voice conversion's z_p = flow(z, y_mask, g), vits.py:1226): the reference's
+    own forward on its fp64 reverse output (the fixture's roundtrip_fp64)."""
+    f, _ = build(meta["config"], meta["seed"], cuda_device, mode)
+    g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
+    z = f(torch.from_numpy(arr["out_ref_fp64"]).float().to(cuda_device), torch.from_numpy(arr["mask"]).to(cuda_device),
+          g=g, reverse=False)
+    assert_close_fp32(z.cpu(), arr["roundtrip_fp64"], f"{name} forward ({mode})", **tol(mode))
+
+
+@pytest.mark.parametrize("num_flows,cond", [(3, 0), (4, 4), (5, 4)])
+def test_vits_flow_forward_vs_oracle_and_roundtrip(cuda_device, num_flows, cond):
+    """Odd and even flow counts (the up-front flip for odd counts), with and without speaker
+    conditioning, against the fp64 oracle; then reverse(forward(x)) = x under the mask."""
+    cfg = dict(VITS_FLOW, channels=64, hidden_channels=96, num_layers=3, num_flows=num_flows, dilation_rate=2,
+               cond_channels=cond)
+    f, sd = build(cfg, 21 + num_flows, cuda_device, "f16x3")
+    gen = torch.Generator().manual_seed(num_flows)
+    B, T = 3, 77
+    x = torch.randn(B, 64, T, generator=gen)
+    m = (torch.arange(T)[None] < torch.tensor([77, 40, 1])[:, None]).float().unsqueeze(1)
+    g = torch.randn(B, cond, 1, generator=gen) if cond else None
+    gd = g.to(cuda_device) if g is not None else None
+    z = f(x.to(cuda_device), m.to(cuda_device), g=gd, reverse=False)
+    zr = vits_ref.vits_flow_forward(sd, x, m, g, **cfg)
+    assert_close_fp32(z.cpu(), zr, f"vits forward F={num_flows}", **tol("f16x3"))
+    y = f(z, m.to(cuda_device), g=gd, reverse=True)
+    assert torch.allclose((y.cpu() * m), x * m, atol=1e-4)
+
+
+# ----------------------------------------------------------------------------- posterior encoder
+POSTERIOR = goldens("vits_posterior")
+
+
+def build_posterior(cfg, seed, device, math_mode):
+    from tts_amd.tts import PosteriorEncoder
+
+    pe = PosteriorEncoder(cfg["in_channels"], cfg["out_channels"], cfg["hidden_channels"], cfg["kernel_size"],
+                          cfg["dilation_rate"], cfg["num_layers"], cond_channels=cfg["cond_channels"],
+                          math_mode=math_mode)
+    sd = synthetic.vits_posterior_state_dict(**cfg, seed=seed)
+    pe.load_state_dict(sd)
+    return pe.to(device), sd
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name,meta,arr", POSTERIOR, ids=[g[0] for g in POSTERIOR])
+def test_vits_posterior_vs_reference(cuda_device, name, meta, arr, mode):
+    """PosteriorEncoder (networks.py:235-288) against the reference's own outputs, with the noise
+    the reference drew (the fixture's eps) passed in."""
+    pe, _ = build_posterior(meta["config"], meta["seed"], cuda_device, mode)
+    g = torch.from_numpy(arr["g"]).to(cuda_device) if "g" in arr else None
+    z, m, logs, mask = pe(torch.from_numpy(arr["x"]).to(cuda_device), torch.from_numpy(arr["lengths"]), g=g,
+                          noise=torch.from_numpy(arr["eps"]))
+    assert torch.equal(mask.cpu(), torch.from_numpy(arr["mask"]))
+    t = tol(mode, op=True)
+    assert_close_fp32(z.cpu(), arr["z_ref_fp64"], f"{name} z ({mode})", **t)
+    assert_close_fp32(m.cpu(), arr["m_ref_fp64"], f"{name} m ({mode})", **t)
+    assert_close_fp32(logs.cpu(), arr["logs_ref_fp64"], f"{name} logs ({mode})", **t)
+
+
+def test_vits_voice_conversion_path(cuda_device):
+    """vits.py:1202-1228 on device: posterior encoder (source speaker) -> flow forward (source g)
+    -> flow reverse (target g), against the fp64 oracle chain with the same noise; the round trip
+    with source = target gives z back."""
+    from tts_amd.config import VITS_POSTERIOR
+
+    cond = 16
+    pcfg = dict(VITS_POSTERIOR, cond_channels=cond, num_layers=4)
+    fcfg = dict(VITS_FLOW, cond_channels=cond)
+    pe, psd = build_posterior(pcfg, 5, cuda_device, "f16x3")
+    flow, fsd = build(fcfg, 6, cuda_device, "f16x3")
+    gen = torch.Generator().manual_seed(8)
+    B, T = 2, 120
+    y = torch.randn(B, 513, T, generator=gen)
+    lengths = torch.tensor([120, 77])
+    eps = torch.randn(B, 192, T, generator=gen)
+    g_src = torch.randn(B, cond, 1, generator=gen)
+    g_tgt = torch.randn(B, cond, 1, generator=gen)
+    z, _, _, mask = pe(y.to(cuda_device), lengths, g=g_src.to(cuda_device), noise=eps)
+    z_p = flow(z, mask, g=g_src.to(cuda_device), reverse=False)
+    z_hat = flow(z_p, mask, g=g_tgt.to(cuda_device), reverse=True)
+    m = mask.cpu()
+    zr, _, _ = vits_ref.vits_posterior(psd, y, m, eps, g_src, **pcfg)
+    zpr = vits_ref.vits_flow_forward(fsd, zr, m, g_src, **fcfg)
+    zhr = vits_ref.vits_flow_reverse(fsd, zpr, m, g_tgt, **fcfg)
+    assert_close_fp32(z.cpu(), zr, "posterior z", **tol("f16x3", op=True))
+    assert_close_fp32(z_p.cpu(), zpr, "z_p", **tol("f16x3", op=True))
+    assert_close_fp32(z_hat.cpu(), zhr, "z_hat", **tol("f16x3", op=True))
+    back = flow(z_p, mask, g=g_src.to(cuda_device), reverse=True)
+    assert torch.allclose(back * mask, z * mask, atol=1e-4)

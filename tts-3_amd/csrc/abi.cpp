@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 111; }
+int tts_abi_version(void) { return 112; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -329,27 +329,29 @@ int tts_glow_decoder_destroy(void* handle) {
 }
 
 int tts_glow_decoder_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g, int B,
-                             int C, int T, int reverse, float* d_y, void* hip_stream) {
+                             int C, int T, int reverse, float* d_y, float* d_logdet, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
-    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
-    static_cast<tts::GlowDecoder*>(handle)->reverse(d_x, d_mask, d_g, B, C, T, d_y,
-                                                    static_cast<hipStream_t>(hip_stream));
+    TTS_REQUIRE(reverse == 0 || reverse == 1, 1, "reverse must be 0 or 1");
+    auto* h = static_cast<tts::GlowDecoder*>(handle);
+    if (reverse) h->reverse(d_x, d_mask, d_g, B, C, T, d_y, static_cast<hipStream_t>(hip_stream));
+    else h->forward(d_x, d_mask, d_g, B, C, T, d_y, d_logdet, static_cast<hipStream_t>(hip_stream));
   });
 }
 
 int tts_glow_decoder_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
-                                      int B, int C, int T, int reverse, float* d_y, void* hip_stream,
-                                      TtsLaunchRecord* records, int max_records, int* n_records) {
+                                      int B, int C, int T, int reverse, float* d_y, float* d_logdet,
+                                      void* hip_stream, TtsLaunchRecord* records, int max_records, int* n_records) {
   return guarded([&] {
     TTS_REQUIRE(handle && n_records, 1, "NULL argument");
-    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    TTS_REQUIRE(reverse == 0 || reverse == 1, 1, "reverse must be 0 or 1");
     auto* h = static_cast<tts::GlowDecoder*>(handle);
     auto s = static_cast<hipStream_t>(hip_stream);
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
+      if (reverse) h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
+      else h->forward(d_x, d_mask, d_g, B, C, T, d_y, d_logdet, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);
@@ -395,8 +397,10 @@ int tts_vits_flow_forward(void* handle, const float* d_x, const float* d_mask, c
                           int T, int reverse, float* d_y, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
-    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
-    static_cast<tts::VitsFlow*>(handle)->reverse(d_x, d_mask, d_g, B, C, T, d_y, static_cast<hipStream_t>(hip_stream));
+    TTS_REQUIRE(reverse == 0 || reverse == 1, 1, "reverse must be 0 or 1");
+    auto* h = static_cast<tts::VitsFlow*>(handle);
+    if (reverse) h->reverse(d_x, d_mask, d_g, B, C, T, d_y, static_cast<hipStream_t>(hip_stream));
+    else h->forward(d_x, d_mask, d_g, B, C, T, d_y, static_cast<hipStream_t>(hip_stream));
   });
 }
 
@@ -405,13 +409,78 @@ int tts_vits_flow_forward_profiled(void* handle, const float* d_x, const float* 
                                    TtsLaunchRecord* records, int max_records, int* n_records) {
   return guarded([&] {
     TTS_REQUIRE(handle && n_records, 1, "NULL argument");
-    TTS_REQUIRE(reverse == 1, 3, "only the reverse (inference) direction is implemented");
+    TTS_REQUIRE(reverse == 0 || reverse == 1, 1, "reverse must be 0 or 1");
     auto* h = static_cast<tts::VitsFlow*>(handle);
     auto s = static_cast<hipStream_t>(hip_stream);
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
+      if (reverse) h->reverse(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
+      else h->forward(d_x, d_mask, d_g, B, C, T, d_y, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+// ----------------------------------------------------------------------------- VITS posterior encoder
+int tts_vits_posterior_num_weights(const TtsVitsPosteriorCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_posterior_validate(*cfg);
+    n = (int)tts::vits_posterior_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_vits_posterior_weight_numel(const TtsVitsPosteriorCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_posterior_validate(*cfg);
+    auto s = tts::vits_posterior_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_vits_posterior_create(const TtsVitsPosteriorCfg* cfg, const float* const* host_weights, int device,
+                              void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::VitsPosterior(*cfg, host_weights, device);
+  });
+}
+
+int tts_vits_posterior_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::VitsPosterior*>(handle); });
+}
+
+int tts_vits_posterior_forward(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                               const float* d_eps, int B, int C, int T, float* d_z, float* d_m, float* d_logs,
+                               void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::VitsPosterior*>(handle)->forward(d_x, d_mask, d_g, d_eps, B, C, T, d_z, d_m, d_logs,
+                                                      static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_posterior_forward_profiled(void* handle, const float* d_x, const float* d_mask, const float* d_g,
+                                        const float* d_eps, int B, int C, int T, float* d_z, float* d_m,
+                                        float* d_logs, void* hip_stream, TtsLaunchRecord* records,
+                                        int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::VitsPosterior*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->forward(d_x, d_mask, d_g, d_eps, B, C, T, d_z, d_m, d_logs, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);

@@ -3,10 +3,39 @@
 // wavenet.py:94-115, normalization.py:88-103.
 #include "glow.hpp"
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
 namespace tts {
+
+// log(det(W)) of an S x S matrix in fp64 (partial-pivot LU); the InvConvNear weight has det > 0
+// (glow.py:94-95); a non-positive determinant is rejected like torch.logdet's NaN / -inf
+double logdet_fp64(const float* w, int S) {
+  std::vector<double> a((size_t)S * S);
+  for (int i = 0; i < S * S; ++i) a[i] = w[i];
+  double ld = 0.0;
+  int sign = 1;
+  for (int k = 0; k < S; ++k) {
+    int p = k;
+    for (int r = k + 1; r < S; ++r)
+      if (std::fabs(a[(size_t)r * S + k]) > std::fabs(a[(size_t)p * S + k])) p = r;
+    if (a[(size_t)p * S + k] == 0.0) throw Error(1, "InvConvNear weight is singular");
+    if (p != k) {
+      for (int c = 0; c < S; ++c) std::swap(a[(size_t)p * S + c], a[(size_t)k * S + c]);
+      sign = -sign;
+    }
+    const double piv = a[(size_t)k * S + k];
+    if (piv < 0) sign = -sign;
+    ld += std::log(std::fabs(piv));
+    for (int r = k + 1; r < S; ++r) {
+      const double f = a[(size_t)r * S + k] / piv;
+      for (int c = k; c < S; ++c) a[(size_t)r * S + c] -= f * a[(size_t)k * S + c];
+    }
+  }
+  TTS_REQUIRE(sign > 0, 1, "InvConvNear weight has a negative determinant (logdet undefined)");
+  return ld;
+}
 
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil) {
   return conv_tile_for(mode, Cout, K, Cin, dil, false);
@@ -46,6 +75,7 @@ std::vector<int64_t> glow_weight_shapes(const TtsGlowDecoderCfg& c) {
     n.push_back(C2);                      // actnorm.logs
     n.push_back(C2);                      // actnorm.bias
     n.push_back((int64_t)S * S);          // invconv.weight_inv
+    n.push_back((int64_t)S * S);          // invconv.weight (the forward direction)
     n.push_back((int64_t)H * (C2 / 2));   // start.weight
     n.push_back(H);                       // start.bias
     if (c.c_in_channels > 0) {            // wn.cond_layer (weight norm folded), wavenet.py:64-66
@@ -142,7 +172,14 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   for (int f = 0; f < cfg_.num_flow_blocks; ++f) {
     Flow& F = flows_[f];
     put(hw[wi], C2, &F.logs); put(hw[wi + 1], C2, &F.bias); put(hw[wi + 2], (size_t)S * S, &F.winv);
-    wi += 3;
+    put(hw[wi + 3], (size_t)S * S, &F.w);
+    {  // forward logdet per unmasked frame: torch.sum(logs) (normalization.py:100) and
+       // torch.logdet(weight) * (C2 / S) (glow.py:128), here in fp64 from the fp32 parameters
+      double sl = 0.0;
+      for (int c = 0; c < C2; ++c) sl += (double)hw[wi][c];
+      F.per_len = sl + logdet_fp64(hw[wi + 3], S) * ((double)C2 / S);
+    }
+    wi += 4;
     put_conv(F.start, hw[wi], hw[wi + 1], C2 / 2, H, 1, 1); wi += 2;
     if (cfg_.c_in_channels > 0) {  // cond_layer stays fp32 [2HL][c_in] (launch_cond_vec)
       put(hw[wi], (size_t)2 * H * L * cfg_.c_in_channels, &F.cond_w);
@@ -184,8 +221,10 @@ void GlowDecoder::reserve(int B, int Th) {
   // xs C2, h H, xin 2H, acts H, rs 2H, skip H, out C2, msq 1; cond vectors [B][2HL]; f16x3: max-abs
   // slot groups
   const size_t cond = cfg_.c_in_channels > 0 ? (size_t)B * 2 * H * cfg_.num_coupling_layers + 64 : 0;
-  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 9 * sizeof(float) +
-                      (cond + amax_floats(B)) * sizeof(float);
+  // forward direction: logdet partials [flows][B][kGlowLogdetParts] fp64
+  const size_t ldp = (size_t)cfg_.num_flow_blocks * B * kGlowLogdetParts * 2 + 64;
+  const size_t need = plane * (2 * C2 + 7 * H + 1) * sizeof(float) + 64 * 10 * sizeof(float) +
+                      (cond + amax_floats(B) + ldp) * sizeof(float);
   if (need <= ws_bytes_) return;
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
   if (hipMalloc(&ws_, need) != hipSuccess) throw Error(4, "hipMalloc(workspace) failed");
@@ -194,6 +233,16 @@ void GlowDecoder::reserve(int B, int Th) {
 
 void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int B, int C, int T, float* y,
                           hipStream_t s, Profiler* prof) {
+  run_flows(true, x, mask, g, B, C, T, y, nullptr, s, prof);
+}
+
+void GlowDecoder::forward(const float* x, const float* mask, const float* g, int B, int C, int T, float* y,
+                          float* logdet, hipStream_t s, Profiler* prof) {
+  run_flows(false, x, mask, g, B, C, T, y, logdet, s, prof);
+}
+
+void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const float* g, int B, int C, int T,
+                            float* y, float* logdet, hipStream_t s, Profiler* prof) {
   TTS_REQUIRE(x && mask && y, 1, "NULL input/output pointer");
   TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1, 1, "batch must be >= 1");
@@ -206,6 +255,7 @@ void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int
   const int C2 = C * nsq;
   const int H = cfg_.hidden_channels;
   const int L = cfg_.num_coupling_layers;
+  const int NF = cfg_.num_flow_blocks;
   const size_t plane = (size_t)B * Th;
   auto al = [](size_t n) { return (n + 63) & ~size_t(63); };
   float* p = ws_;
@@ -221,6 +271,8 @@ void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int
   if (cfg_.c_in_channels > 0) { cvec = p; p += al((size_t)B * 2 * H * L); }
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
   unsigned* amax = h3 ? reinterpret_cast<unsigned*>(p) : nullptr;
+  p += al(amax_floats(B));
+  double* ldp = reinterpret_cast<double*>(p);  // forward: logdet partials [NF][B][npb]
   const int ng = 2 * L + 2;
   // slot group: flow fi (execution order), kind 0 = x0, 1 + l = h_l, 1 + L + l = acts_l, 2L + 1 = skip
   auto slots = [&](int fi, int kind) -> unsigned* { return h3 ? amax + ((size_t)fi * ng + kind) * B * 64 : nullptr; };
@@ -250,14 +302,15 @@ void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int
         [&] { launch_conv(cfg_.math_mode, a, B, cv.K, cv.tile, s); });
   };
 
-  // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1
-  for (int f = cfg_.num_flow_blocks - 1; f >= 0; --f) {
-    const Flow& F = flows_[f];
-    const int fi = cfg_.num_flow_blocks - 1 - f;
+  // out = end(WN(start(x_0) * mask, mask, g)) of flow block f (glow.py:212-214); fi = execution index
+  // x0 statistics: the max-abs slots of flow fi's start-conv input come from the previous
+  // elementwise kernel (the tail / head / coupling kernels) except for the first reverse flow, or
+  // from a strided pre-pass for every flow (TTS_MI355X_FLOW_AMAX_PREPASS=1)
+  auto coupling_net = [&](const Flow& F, int fi) {
     if (cvec)  // g = cond_layer(g) (wavenet.py:98-99); every flow has its own cond_layer
       run(prof, s, "glow_cond", 2.0 * B * 2 * H * L * cfg_.c_in_channels, 4.0 * B * 2 * H * L,
           [&] { launch_cond_vec(g, F.cond_w, F.cond_b, cvec, B, cfg_.c_in_channels, 2 * H * L, s); });
-    if (h3 && (fi == 0 || amax_prepass_))  // statistics of x_0 (the start conv's input); later flows: the previous tail
+    if (h3 && ((rev && fi == 0) || amax_prepass_))
       run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
@@ -278,12 +331,49 @@ void GlowDecoder::reverse(const float* x, const float* mask, const float* g, int
                               l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
       });  // :110-115
     }
-    conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));        // glow.py:214
-    GlowTailArgs ta{};
-    ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
-    ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
-    ta.amax_x0 = (h3 && f > 0 && !amax_prepass_) ? slots(fi + 1, 0) : nullptr;
-    run(prof, s, "glow_tail", 0.0, 16.0 * P * C2, [&] { launch_glow_tail(ta, B, s); });
+    conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));  // glow.py:214
+  };
+
+  if (rev) {
+    // flows in reverse: for each block (last first): CouplingBlock^-1, InvConvNear^-1, ActNorm^-1
+    for (int f = NF - 1; f >= 0; --f) {
+      const Flow& F = flows_[f];
+      const int fi = NF - 1 - f;
+      coupling_net(F, fi);
+      GlowTailArgs ta{};
+      ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
+      ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;
+      ta.amax_x0 = (h3 && f > 0 && !amax_prepass_) ? slots(fi + 1, 0) : nullptr;
+      run(prof, s, "glow_tail", 0.0, 16.0 * P * C2, [&] { launch_glow_tail(ta, B, s); });
+    }
+  } else {
+    // flows in order (decoder.py:119-133): ActNorm, InvConvNear, CouplingBlock per block; the head of
+    // block 0 runs alone, every later head inside the previous block's coupling kernel
+    GlowHeadArgs ha{};
+    ha.x = xs; ha.mask = msq; ha.w = flows_[0].w; ha.logs = flows_[0].logs; ha.bias = flows_[0].bias;
+    ha.C2 = C2; ha.Th = Th; ha.S = cfg_.num_splits;
+    ha.amax_x0 = (h3 && !amax_prepass_) ? slots(0, 0) : nullptr;
+    run(prof, s, "glow_head", 0.0, 8.0 * P * C2, [&] { launch_glow_head(ha, B, s); });
+    const int npb = glow_couple_parts(C2, cfg_.num_splits, Th);
+    double per_len = 0.0;
+    for (int f = 0; f < NF; ++f) {
+      const Flow& F = flows_[f];
+      per_len += F.per_len;
+      coupling_net(F, f);
+      GlowCoupleArgs ca{};
+      ca.x = xs; ca.out = out; ca.mask = msq; ca.C2 = C2; ca.Th = Th; ca.S = cfg_.num_splits;
+      ca.sigmoid_scale = cfg_.sigmoid_scale;
+      ca.ld_part = logdet ? ldp + (size_t)f * B * npb : nullptr;
+      if (f + 1 < NF) {
+        ca.w = flows_[f + 1].w; ca.logs = flows_[f + 1].logs; ca.bias = flows_[f + 1].bias;
+        ca.amax_x0 = (h3 && !amax_prepass_) ? slots(f + 1, 0) : nullptr;
+      }
+      run(prof, s, f + 1 < NF ? "glow_couple_head" : "glow_couple", 0.0, 16.0 * P * C2,
+          [&] { launch_glow_couple_fwd(ca, B, s); });
+    }
+    if (logdet)
+      run(prof, s, "glow_logdet", 0.0, 8.0 * B * NF * npb + 4.0 * P,
+          [&] { launch_glow_logdet(ldp, NF, npb, msq, Th, per_len, logdet, B, s); });
   }
   if (nsq > 1) {
     run(prof, s, "glow_unsqueeze", 0.0, 8.0 * P * C2 + 4.0 * P,

@@ -53,6 +53,34 @@ void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipSt
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,
                            int Th, int first, int last, hipStream_t s, unsigned* amax = nullptr);
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s);
+// forward direction (reverse=False)
+struct GlowHeadArgs {  // ActNorm -> InvConvNear forward of one flow block, in place
+  float* x;            // [B][C2][Th]
+  const float* mask;   // [B][Th]
+  const float* w;      // [S][S] InvConvNear weight (glow.py:97-100)
+  const float* logs;   // [C2]
+  const float* bias;   // [C2]
+  int C2, Th, S;
+  unsigned* amax_x0;   // f16x3 statistics of x[:, :C2/2] after the update, or nullptr
+};
+struct GlowCoupleArgs {  // coupling forward of one block, then (w != nullptr) the next block's head
+  float* x;
+  const float* out;    // end(WN(...)): rows [0,C2/2) = t, [C2/2,C2) = s
+  const float* mask;
+  int C2, Th, S;
+  int sigmoid_scale;
+  double* ld_part;     // [B][glow_couple_parts()] partial sums of s * mask, or nullptr
+  const float* w;      // next block's head (nullptr: none)
+  const float* logs;
+  const float* bias;
+  unsigned* amax_x0;
+};
+constexpr int kGlowLogdetParts = 128;  // at most this many workgroups (logdet partials) per utterance
+void launch_glow_head(const GlowHeadArgs& a, int B, hipStream_t s);
+int glow_couple_parts(int C2, int S, int Th);
+void launch_glow_couple_fwd(const GlowCoupleArgs& a, int B, hipStream_t s);
+void launch_glow_logdet(const double* parts, int nparts, int npb, const float* mask, int Th, double per_len,
+                        float* logdet, int B, hipStream_t s);
 void launch_channel_flip(const float* x, float* y, int B, int C, int T, hipStream_t s);  // torch.flip(x, [1])
 
 class GlowDecoder {
@@ -64,6 +92,9 @@ class GlowDecoder {
   // g: [B][c_in_channels] speaker vector (the reference's g [B][c_in][1]), NULL when c_in_channels == 0
   void reverse(const float* x, const float* mask, const float* g, int B, int C, int T, float* y, hipStream_t s,
                Profiler* prof = nullptr);
+  // reverse=False (decoder.py:119-133): y = the flows in order, logdet[B] (fp32, nullptr: not computed)
+  void forward(const float* x, const float* mask, const float* g, int B, int C, int T, float* y, float* logdet,
+               hipStream_t s, Profiler* prof = nullptr);
   int device() const { return device_; }
 
  private:
@@ -77,11 +108,15 @@ class GlowDecoder {
     float* logs = nullptr;
     float* bias = nullptr;
     float* winv = nullptr;
+    float* w = nullptr;       // InvConvNear weight (forward direction)
+    double per_len = 0.0;     // sum(logs) + logdet(W) * C2 / S: the block's logdet per unmasked frame
     float* cond_w = nullptr;  // wn.cond_layer [2HL][c_in] fp32 (c_in_channels > 0)
     float* cond_b = nullptr;
     Conv start, end;
     std::vector<Conv> in_layers, res_skip;
   };
+  void run_flows(bool rev, const float* x, const float* mask, const float* g, int B, int C, int T, float* y,
+                 float* logdet, hipStream_t s, Profiler* prof);
   void reserve(int B, int Th);
   size_t amax_floats(int B) const;
 

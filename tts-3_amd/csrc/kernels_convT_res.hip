@@ -81,19 +81,13 @@ __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
       const int rr = u >> 2;
       if (rr < NG * P::XROWS) {
         const int g = rr / P::XROWS, r = rr - (rr / P::XROWS) * P::XROWS;
-        u16x4 pv[NP];
+        float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          unsigned short h[NP];
-          float v = lrelu2(xr[i][j], a.in_slope);
-          if (H3) v *= xscale;
-          S::split(v, h);
-#pragma unroll
-          for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+          v[j] = lrelu2(xr[i][j], a.in_slope);
+          if (H3) v[j] *= xscale;
         }
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-          *reinterpret_cast<u16x4*>(smem + (g * P::XROWS + r) * S::ROWB + 8 * q + 32 * p) = pv[p];
+        split_store4<S>(smem + (g * P::XROWS + r) * S::ROWB + 8 * q, v[0], v[1], v[2], v[3]);
       }
     }
   }

@@ -5,6 +5,10 @@
 //   tail                     glow.py:222-224 (coupling affine inverse) -> glow.py:102-137
 //                            (InvConvNear inverse) -> normalization.py:96-98 (ActNorm inverse),
 //                            fused: one thread owns the S channels InvConvNear mixes.
+//   forward direction (reverse=False, decoder.py:119-133): head = ActNorm -> InvConvNear of one
+//   flow block (normalization.py:99-100, glow.py:126-135); couple_fwd = the coupling affine
+//   (glow.py:225-227) fused with the next block's head; the logdet terms sum per utterance in
+//   fixed order (partials per workgroup, then glow_logdet_kernel).
 #include "glow.hpp"
 #include "conv_device.hpp"
 
@@ -136,6 +140,132 @@ __global__ __launch_bounds__(256) void glow_tail_kernel(GlowTailArgs a) {
   if (a.amax_x0) publish_amax_block(a.amax_x0, b, vm);
 }
 
+// ActNorm forward then InvConvNear forward of one flow block on the S channels of group i, in
+// registers: v = (bias + exp(logs) * x) * mask; z = W . v * mask.  Returns |z_0| max contribution.
+template <int S>
+__device__ __forceinline__ float glow_head_group(float (&z)[S], const int (&chs)[S], const float (&W)[S][S],
+                                                 const float* logs, const float* bias, float m, int half) {
+  float v[S];
+#pragma unroll
+  for (int g = 0; g < S; ++g) v[g] = (bias[chs[g]] + expf(logs[chs[g]]) * z[g]) * m;  // ActNorm (:99)
+  float vm = 0.f;
+#pragma unroll
+  for (int o = 0; o < S; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int g = 0; g < S; ++g) acc = fmaf(W[o][g], v[g], acc);
+    z[o] = acc * m;  // InvConvNear: conv2d, then * x_mask (glow.py:132-135)
+    if (chs[o] < half) vm = fmaxf(vm, fabsf(z[o]));
+  }
+  return vm;
+}
+
+// Block sum (256 threads) of a double, fixed order; thread 0 returns it
+__device__ __forceinline__ double block_sum_d(double v) {
+  __shared__ double red[256];
+  red[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+// Flow block 0's head (the later heads run inside glow_couple_fwd_kernel)
+template <int S>
+__global__ __launch_bounds__(256) void glow_head_kernel(GlowHeadArgs a) {
+  const int b = blockIdx.y;
+  const int C2 = a.C2, Th = a.Th, half = C2 / 2;
+  const int64_t n = (int64_t)(C2 / S) * Th;
+  float W[S][S];
+#pragma unroll
+  for (int o = 0; o < S; ++o)
+#pragma unroll
+    for (int g = 0; g < S; ++g) W[o][g] = a.w[o * S + g];
+  float vm = 0.f;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e % Th), i = (int)(e / Th);
+    const float m = a.mask[(size_t)b * Th + t];
+    float z[S];
+    int chs[S];
+#pragma unroll
+    for (int g = 0; g < S; ++g) {
+      chs[g] = (g / (S / 2)) * half + i * (S / 2) + g % (S / 2);
+      z[g] = a.x[((size_t)b * C2 + chs[g]) * Th + t];
+    }
+    vm = fmaxf(vm, glow_head_group<S>(z, chs, W, a.logs, a.bias, m, half));
+#pragma unroll
+    for (int g = 0; g < S; ++g) a.x[((size_t)b * C2 + chs[g]) * Th + t] = z[g];
+  }
+  if (a.amax_x0) publish_amax_block(a.amax_x0, b, vm);
+}
+
+// Coupling forward (glow.py:216-227): z_1 = (t + exp(s) * x_1) * mask, logdet partial sum(s * mask);
+// then, when a.w != nullptr, the next flow block's head on the same S channels
+template <int S>
+__global__ __launch_bounds__(256) void glow_couple_fwd_kernel(GlowCoupleArgs a) {
+  const int b = blockIdx.y;
+  const int C2 = a.C2, Th = a.Th, half = C2 / 2;
+  const int64_t n = (int64_t)(C2 / S) * Th;
+  const bool head = a.w != nullptr;
+  float W[S][S];
+#pragma unroll
+  for (int o = 0; o < S; ++o)
+#pragma unroll
+    for (int g = 0; g < S; ++g) W[o][g] = head ? a.w[o * S + g] : 0.f;
+  float vm = 0.f;
+  double ld = 0.0;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e % Th), i = (int)(e / Th);
+    const float m = a.mask[(size_t)b * Th + t];
+    float z[S];
+    int chs[S];
+#pragma unroll
+    for (int g = 0; g < S; ++g) {
+      const int ch = (g / (S / 2)) * half + i * (S / 2) + g % (S / 2);
+      chs[g] = ch;
+      const float xv = a.x[((size_t)b * C2 + ch) * Th + t];
+      if (ch < half) {
+        z[g] = xv;  // z_0 = x_0
+      } else {
+        const float tt = a.out[((size_t)b * C2 + (ch - half)) * Th + t];
+        float sv = a.out[((size_t)b * C2 + ch) * Th + t];
+        if (a.sigmoid_scale) sv = logf(1e-6f + 1.f / (1.f + expf(-(sv + 2.f))));
+        z[g] = (tt + expf(sv) * xv) * m;  // z_1 = (t + exp(s) * x_1) * x_mask
+        ld += (double)(sv * m);           // torch.sum(s * x_mask, [1, 2])
+      }
+    }
+    if (head) vm = fmaxf(vm, glow_head_group<S>(z, chs, W, a.logs, a.bias, m, half));
+#pragma unroll
+    for (int g = 0; g < S; ++g) a.x[((size_t)b * C2 + chs[g]) * Th + t] = z[g];
+  }
+  if (a.ld_part) {
+    const double tot = block_sum_d(ld);
+    if (threadIdx.x == 0) a.ld_part[(size_t)b * gridDim.x + blockIdx.x] = tot;
+  }
+  if (head && a.amax_x0) publish_amax_block(a.amax_x0, b, vm);
+}
+
+// logdet[b] = per_len * x_len[b] + sum of the coupling partials [nparts][B][npb] (fixed order, fp64);
+// x_len = sum_t mask[b][t] (normalization.py:91, glow.py:122); per_len = sum over flow blocks of
+// sum(logs) + logdet(W) * C2 / S (the ActNorm and InvConvNear terms)
+__global__ __launch_bounds__(256) void glow_logdet_kernel(const double* parts, int nparts, int npb, const float* mask,
+                                                          int Th, double per_len, float* logdet, int B) {
+  const int b = blockIdx.x;
+  double xl = 0.0, ps = 0.0;
+  for (int t = threadIdx.x; t < Th; t += 256) xl += (double)mask[(size_t)b * Th + t];
+  for (int k = threadIdx.x; k < nparts * npb; k += 256) {
+    const int f = k / npb, j = k - f * npb;
+    ps += parts[((size_t)f * B + b) * npb + j];
+  }
+  xl = block_sum_d(xl);
+  __syncthreads();
+  ps = block_sum_d(ps);
+  if (threadIdx.x == 0) logdet[b] = (float)(per_len * xl + ps);
+}
+
 namespace {
 dim3 ew_grid(int64_t n, int B, int64_t cap = 4096) {
   int64_t g = (n + 255) / 256;
@@ -190,6 +320,40 @@ void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* 
   TTS_HIP_CHECK(hipGetLastError());
 }
 
+void launch_glow_head(const GlowHeadArgs& a, int B, hipStream_t s) {
+  const int64_t n = (int64_t)(a.C2 / a.S) * a.Th;
+  const int64_t cap = a.amax_x0 ? 128 : 4096;
+  switch (a.S) {
+    case 2: hipLaunchKernelGGL(glow_head_kernel<2>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(glow_head_kernel<4>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(glow_head_kernel<8>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
+    default: throw Error(3, "InvConvNear num_splits must be 2, 4 or 8");
+  }
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+int glow_couple_parts(int C2, int S, int Th) {
+  return (int)ew_grid((int64_t)(C2 / S) * Th, 1, kGlowLogdetParts).x;
+}
+
+void launch_glow_couple_fwd(const GlowCoupleArgs& a, int B, hipStream_t s) {
+  const int64_t n = (int64_t)(a.C2 / a.S) * a.Th;
+  const dim3 grid = ew_grid(n, B, kGlowLogdetParts);  // fixed per shape: the logdet sums are deterministic
+  switch (a.S) {
+    case 2: hipLaunchKernelGGL(glow_couple_fwd_kernel<2>, grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(glow_couple_fwd_kernel<4>, grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(glow_couple_fwd_kernel<8>, grid, dim3(256), 0, s, a); break;
+    default: throw Error(3, "InvConvNear num_splits must be 2, 4 or 8");
+  }
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+void launch_glow_logdet(const double* parts, int nparts, int npb, const float* mask, int Th, double per_len,
+                        float* logdet, int B, hipStream_t s) {
+  hipLaunchKernelGGL(glow_logdet_kernel, dim3(B), dim3(256), 0, s, parts, nparts, npb, mask, Th, per_len, logdet, B);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s) {
   const int64_t n = (int64_t)(a.C2 / a.S) * a.Th;
   const int64_t cap = a.amax_x0 ? 128 : 4096;  // with statistics: one atomic per workgroup, <= 128 per item
@@ -199,6 +363,40 @@ void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s) {
     case 8: hipLaunchKernelGGL(glow_tail_kernel<8>, ew_grid(n, B, cap), dim3(256), 0, s, a); break;
     default: throw Error(3, "InvConvNear num_splits must be 2, 4 or 8");
   }
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tts
+
+// ---------------------------------------------------------------------------------------------
+// VITS PosteriorEncoder sample (networks.py:286-287): m, logs = split(stats); z = (m + eps *
+// exp(logs)) * mask.  stats = proj(x) * mask is already masked.
+#include "vits.hpp"
+
+namespace tts {
+
+__global__ __launch_bounds__(256) void posterior_sample_kernel(const float* stats, const float* eps,
+                                                               const float* mask, float* z, float* m, float* logs,
+                                                               int Co, int T) {
+  const int b = blockIdx.y;
+  const int64_t n = (int64_t)Co * T;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int t = (int)(i % T);
+    const float mv = stats[(size_t)b * 2 * n + i];
+    const float lv = stats[(size_t)b * 2 * n + n + i];
+    const float e = eps ? eps[(size_t)b * n + i] : 0.f;
+    z[(size_t)b * n + i] = (mv + e * expf(lv)) * mask[(size_t)b * T + t];
+    if (m) m[(size_t)b * n + i] = mv;
+    if (logs) logs[(size_t)b * n + i] = lv;
+  }
+}
+
+void launch_posterior_sample(const float* stats, const float* eps, const float* mask, float* z, float* m,
+                             float* logs, int B, int Co, int T, hipStream_t s) {
+  int64_t g = ((int64_t)Co * T + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(posterior_sample_kernel, dim3((unsigned)g, B), dim3(256), 0, s, stats, eps, mask, z, m, logs,
+                     Co, T);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

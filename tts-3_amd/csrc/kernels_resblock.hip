@@ -115,18 +115,13 @@ void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
     for (int i = 0; i < P::UPT; ++i) {
       if (ulds[i] >= 0) {
-        u16x4 pv[NP];
+        float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          unsigned short h[NP];
-          float v = lrelu2(xreg[i][j], a1.in_slope);
-          if (H3) v *= xscale;
-          S::split(v, h);
-#pragma unroll
-          for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+          v[j] = lrelu2(xreg[i][j], a1.in_slope);
+          if (H3) v[j] *= xscale;
         }
-#pragma unroll
-        for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(xl + ulds[i] + 32 * p) = pv[p];
+        split_store4<S>(xl + ulds[i], v[0], v[1], v[2], v[3]);
       }
     }
   };
@@ -261,13 +256,12 @@ void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          unsigned short h0[NP], h1[NP];
-          S::split(acc[m][n][r] * tscale, h0);
-          S::split(acc[m][n][r + 1] * tscale, h1);
+          unsigned w[NP];
+          S::split2(acc[m][n][r] * tscale, acc[m][n][r + 1] * tscale, w);
           unsigned char* dst = smem + ((co >> 4) * P::TROWS + row) * S::ROWB + 2 * (co & 15);
 #pragma unroll
           for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<unsigned*>(dst + 32 * p) = (unsigned)h0[p] | ((unsigned)h1[p] << 16);
+            *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];
         }
       }
     // zero rows RP_W .. TROWS-1 of every group (read only by the discarded columns)
@@ -510,18 +504,13 @@ void resblock3_kernel(ResBlock3Args a) {
         const int q = u & 3;
         const int r = u >> 2;
         if (r < PR) {
-          u16x4 pv[NP];
+          float v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            unsigned short h[NP];
-            float v = lrelu2(xv[g][i][j], 0.1f);
-            if (H3) v *= xs;
-            S::split(v, h);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+            v[j] = lrelu2(xv[g][i][j], 0.1f);
+            if (H3) v[j] *= xs;
           }
-#pragma unroll
-          for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(smem + (g * PR + r) * S::ROWB + 8 * q + 32 * p) = pv[p];
+          split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * q, v[0], v[1], v[2], v[3]);
         }
       }
 #pragma unroll
@@ -627,13 +616,12 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          unsigned short h0[NP], h1[NP];
-          S::split(acc[m][n][r] * scale, h0);
-          S::split(acc[m][n][r + 1] * scale, h1);
+          unsigned w[NP];
+          S::split2(acc[m][n][r] * scale, acc[m][n][r + 1] * scale, w);
           unsigned char* dst = smem + ((co >> 4) * PR + row) * S::ROWB + 2 * (co & 15);
 #pragma unroll
           for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<unsigned*>(dst + 32 * p) = (unsigned)h0[p] | ((unsigned)h1[p] << 16);
+            *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];
         }
       }
     // edge rows: [0, roff) and [roff + RP_W, PR) of every group

@@ -181,7 +181,19 @@ int pack_conv1d_wino(int mode, const float* w, int Cout, int Cin, int K, const C
         dst[c * kWinoPoints + p] = (float)(kWinoGc[p] * acc);
       }
   }
-  return pack_conv1d_split(mode, wt.data(), Cout, Cin, KS, t, out);
+  // channel order within each 16-channel group: the transform jobs store channels 4q + 2jp + e
+  // (quad q, pair jp, e = 0, 1) at 16-bit position 2 (q + 4 jp) + e of the staged row, so that a
+  // 32-lane store covers all banks; the MFMA k index runs over those positions
+  TTS_REQUIRE(Cin % 16 == 0, 1, "winograd packing: Cin must be a multiple of 16");
+  std::vector<float> wp(wt.size());
+  for (int64_t o = 0; o < Cout; ++o)
+    for (int g = 0; g < Cin / 16; ++g)
+      for (int kk = 0; kk < 16; ++kk) {
+        const int jp = kk >> 3, q = (kk >> 1) & 3, e = kk & 1;
+        const int ch = 4 * q + 2 * jp + e;
+        std::copy_n(wt.data() + ((size_t)o * Cin + g * 16 + ch) * KS, KS, wp.data() + ((size_t)o * Cin + g * 16 + kk) * KS);
+      }
+  return pack_conv1d_split(mode, wp.data(), Cout, Cin, KS, t, out);
 }
 
 }  // namespace tts

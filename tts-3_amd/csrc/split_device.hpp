@@ -10,6 +10,7 @@ namespace tts {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ unsigned short bf16_bits(__bf16 h) { return __builtin_bit_cast(unsigned short, h); }
 __device__ __forceinline__ unsigned short f16_bits(_Float16 h) { return __builtin_bit_cast(unsigned short, h); }
@@ -33,6 +34,13 @@ struct SchemeX6 {
     p[1] = bf16_bits(a1);
     p[2] = bf16_bits((__bf16)r2);
   }
+  __device__ static __forceinline__ void split2(float x0, float x1, unsigned (&w)[3]) {
+    unsigned short a[3], b[3];
+    split(x0, a);
+    split(x1, b);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) w[p] = (unsigned)a[p] | ((unsigned)b[p] << 16);
+  }
   __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
   }
@@ -53,6 +61,21 @@ struct SchemeH3 {
     p[0] = f16_bits(h);
     p[1] = f16_bits((_Float16)(x - (float)h));
   }
+  // two values -> (hi pair, lo pair) words, the same bits as split(): hi = v_cvt_pk_f16_f32 (round
+  // to nearest even); the remainders x - hi are exact in fp32 and v_fma_mix_f32 forms them straight
+  // from the packed fp16 halves (-hi * 1 + x, one rounding of an exact value), so a pair costs 4
+  // VALU instead of 6 (two v_cvt_f32_f16 + two v_sub_f32)
+  __device__ static __forceinline__ void split2(float x0, float x1, unsigned (&w)[2]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 h = __builtin_convertvector((f2){x0, x1}, h2);
+    const unsigned hb = __builtin_bit_cast(unsigned, h);
+    float r0, r1;
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(hb), "v"(x0));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(hb), "v"(x1));
+    w[0] = hb;
+    w[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){r0, r1}, h2));
+  }
   __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
   }
@@ -69,10 +92,23 @@ struct SchemeB1 {
   static constexpr int PACC[1] = {0};
   static constexpr bool SCALED = false;
   __device__ static __forceinline__ void split(float x, unsigned short (&p)[1]) { p[0] = bf16_bits((__bf16)x); }
+  __device__ static __forceinline__ void split2(float x0, float x1, unsigned (&w)[1]) {
+    w[0] = (unsigned)bf16_bits((__bf16)x0) | ((unsigned)bf16_bits((__bf16)x1) << 16);
+  }
   __device__ static __forceinline__ f32x16 mfma(f32x4 a, f32x4 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
   }
 };
+
+// 4 consecutive channels of one staged row -> the pieces' 8-byte slots (dst + 32 p)
+template <class S>
+__device__ __forceinline__ void split_store4(unsigned char* dst, float v0, float v1, float v2, float v3) {
+  unsigned w0[S::NP], w1[S::NP];
+  S::split2(v0, v1, w0);
+  S::split2(v2, v3, w1);
+#pragma unroll
+  for (int p = 0; p < S::NP; ++p) *reinterpret_cast<u32x2*>(dst + 32 * p) = u32x2{w0[p], w1[p]};
+}
 
 // Exponent e such that max|x| * 2^-e lies in [2^13, 2^14): read the 64 max-abs slots the
 // producer published (one per lane), wave max, frexp.  No statistics, zero or non-finite max:

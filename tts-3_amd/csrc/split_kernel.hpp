@@ -168,18 +168,13 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
 #pragma unroll
     for (int i = 0; i < C::UPT; ++i) {
       if (ulds[i] >= 0) {
-        u16x4 pv[NP];
+        float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          unsigned short h[NP];
-          float v = lrelu2(xreg[i][j], slope);
-          if (H3) v *= xscale;
-          S::split(v, h);
-#pragma unroll
-          for (int p = 0; p < NP; ++p) pv[p][j] = h[p];
+          v[j] = lrelu2(xreg[i][j], slope);
+          if (H3) v[j] *= xscale;
         }
-#pragma unroll
-        for (int p = 0; p < NP; ++p) *reinterpret_cast<u16x4*>(xl + ulds[i] + 32 * p) = pv[p];
+        split_store4<S>(xl + ulds[i], v[0], v[1], v[2], v[3]);
       }
     }
   };

@@ -55,7 +55,7 @@ struct Wino8Cfg {
   static constexpr int ROFF = (4 - PAD % 4) % 4;
   static constexpr int RSPAN = (XROWS - 1) % D + 4 * D * ((XROWS - 1) / D) + 6 * D + ROFF + 1;
   static constexpr int RSPAN4 = (RSPAN + 3) / 4 * 4;
-  static constexpr int RPITCH = RSPAN4 % 8 == 4 ? RSPAN4 : RSPAN4 + 4;  // 4*RPITCH = 16 mod 32 banks
+  static constexpr int RPITCH = RSPAN4 % 8 == 4 ? RSPAN4 : RSPAN4 + 4;  // RPITCH / 4 odd
   static constexpr int RF4 = (16 * RPITCH / 4 + 63) / 64 * 64;          // float4s per raw buffer (DMA rows of 64)
   static constexpr int RSZ = RF4 * 16;
   static constexpr int NDMA = RF4 / 64;              // DMA instructions per chunk (waves 4-7)
@@ -149,6 +149,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const int ujj = urow / D, urho = urow - (urow / D) * D;
   const int uri = urho + 4 * D * ujj + C::ROFF;  // raw index of the column's first input
   float tkeep[7], jraw[7];
+  // D = 1: a column's 7 inputs are raw floats 4 urow + ROFF ... + 6 of its channel row, read as NU
+  // aligned float4s (ds_read_b128).  The lanes of a 16-lane group hold 4 columns x 4 channel quads:
+  // float4 slots c * RPITCH / 4 + urow, RPITCH / 4 odd, cover all 16 slots of the bank row (no
+  // conflict), where 7 ds_read_b32 at one sub-offset put 32 lanes on 8 banks (4-way)
+  constexpr int NU = (C::ROFF + 6) / 4 + 1;
+  f32x4 jraw4[NU];
   // piece j: channel 4q + j; pairs are written after channels 1 and 3.  A piece runs in two parts
   // one MFMA step apart: job_load issues its 7 LDS reads, job_finish transforms (and splits and
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
@@ -157,9 +163,16 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   auto job_load = [&](int rb, int j) {
     if (SPREAD && grp == 1 && j >= 2) return;
     if (!uok) return;
-    const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::RPITCH + uri;
+    if constexpr (D == 1) {
+      const f32x4* raw4 =
+          reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * (C::RPITCH / 4) + urow;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) jraw[k] = raw[D * k];
+      for (int u4 = 0; u4 < NU; ++u4) jraw4[u4] = raw4[u4];
+    } else {
+      const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::RPITCH + uri;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) jraw[k] = raw[D * k];
+    }
   };
   auto job_finish = [&](int tb, int j) {
     if (SPREAD && grp == 1 && j >= 2) return;
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     float v[7], t[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      float x = jraw[k];
+      float x = D == 1 ? jraw4[(C::ROFF + k) / 4][(C::ROFF + k) % 4] : jraw[k];
       if (LRELU) x = lrelu2(x, slope);
       v[k] = H3 ? x * xscale : x;
     }
@@ -177,7 +190,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       for (int k = 0; k < 7; ++k) tkeep[k] = t[k];
       return;
     }
-    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 8 * uq + 4 * (piece(j) >> 1);
+    // word uq + 4 * pair of the row (channels 4 uq + 2 pair, +1; the weights are packed in this
+    // channel order, pack_conv1d_wino): a 32-lane half (8 rows x 4 quads) covers all 32 banks
+    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 4 * uq + 16 * (piece(j) >> 1);
 #pragma unroll
     for (int p = 0; p < kWinoPoints; ++p) {
       unsigned w[NP];

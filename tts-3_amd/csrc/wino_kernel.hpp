@@ -68,22 +68,7 @@ __host__ __device__ inline void wino_at(const float (&m)[7], float (&y)[4]) {
 // two values -> NP 32-bit words (piece p of value 0 in the low half, of value 1 in the high half)
 template <class S>
 __device__ __forceinline__ void split_pair(float x0, float x1, unsigned (&w)[S::NP]) {
-  if constexpr (S::SCALED) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const f2 v = {x0, x1};
-    const h2 h = __builtin_convertvector(v, h2);  // v_cvt_pk_f16_f32 (round to nearest even)
-    const f2 hb = __builtin_convertvector(h, f2);
-    const f2 r = {x0 - hb[0], x1 - hb[1]};
-    w[0] = __builtin_bit_cast(unsigned, h);
-    w[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, h2));
-  } else {
-    unsigned short a[S::NP], b[S::NP];
-    S::split(x0, a);
-    S::split(x1, b);
-#pragma unroll
-    for (int p = 0; p < S::NP; ++p) w[p] = (unsigned)a[p] | ((unsigned)b[p] << 16);
-  }
+  S::split2(x0, x1, w);
 }
 
 template <class S, int NCH, int D, int TN>
@@ -318,7 +303,7 @@ __global__ __launch_bounds__(256, TN == 1 ? 2 : 1) void conv1d_wino_kernel(Conv1
       const int ts = tb + D * k;
       uvoff[i][k] = (u < C::UNITS && ts >= 0 && ts < Tin) ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
     }
-    ulds[i] = u < C::UNITS ? row * S::ROWB + 8 * q : -1;
+    ulds[i] = u < C::UNITS ? row * S::ROWB + 4 * q : -1;  // word q + 4 jp (pack_conv1d_wino order)
   }
 
   float xr[C::UPT][4][7];
@@ -347,7 +332,7 @@ __global__ __launch_bounds__(256, TN == 1 ? 2 : 1) void conv1d_wino_kernel(Conv1
       }
       wino_bt(v, t[h]);
     }
-    unsigned char* base = smem + buf * C::XSZB + ulds[i] + 4 * jp;
+    unsigned char* base = smem + buf * C::XSZB + ulds[i] + 16 * jp;
 #pragma unroll
     for (int p = 0; p < NPT; ++p) {
       unsigned w[NP];

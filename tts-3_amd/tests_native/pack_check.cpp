@@ -16,6 +16,7 @@
 
 #include "common.hpp"
 #include "wino_consts.hpp"
+#include <algorithm>
 
 using namespace tts;
 
@@ -162,7 +163,14 @@ static void check_wino(int Cout, int Cin, int K, const ConvTile& t) {
         }
         u[oc * KS + c * kWinoPoints + p] = (float)(kWinoGc[p] * acc);
       }
-  check_split(MATH_FP32_F16X3, u, Cout, Cin, KS, t, out, e, "pack_conv1d_wino");
+  // the packed k position kk of a 16-channel group holds channel 4q + 2jp + e (kk = 8jp + 2q + e)
+  std::vector<float> up(u.size());
+  for (int o = 0; o < Cout; ++o)
+    for (int ci = 0; ci < Cin; ++ci) {
+      const int kk = ci & 15, ch = (ci & ~15) + 4 * ((kk >> 1) & 3) + 2 * (kk >> 3) + (kk & 1);
+      std::copy_n(u.data() + ((size_t)o * Cin + ch) * KS, KS, up.data() + ((size_t)o * Cin + ci) * KS);
+    }
+  check_split(MATH_FP32_F16X3, up, Cout, Cin, KS, t, out, e, "pack_conv1d_wino");
 }
 
 int main() {

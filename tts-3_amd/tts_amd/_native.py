@@ -29,7 +29,7 @@ TTS_ERR_OOM = 4
 MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
 # the C-ABI revision these bindings were written for (tts_abi_version() in csrc/abi.cpp)
-ABI_VERSION = 111
+ABI_VERSION = 112
 
 
 def default_math_mode(fp32_faithful_only: bool = True) -> str:
@@ -130,6 +130,19 @@ class TtsVitsFlowCfg(Structure):
     ]
 
 
+class TtsVitsPosteriorCfg(Structure):
+    _fields_ = [
+        ("in_channels", c_int),
+        ("out_channels", c_int),
+        ("hidden_channels", c_int),
+        ("kernel_size", c_int),
+        ("dilation_rate", c_int),
+        ("num_layers", c_int),
+        ("cond_channels", c_int),
+        ("math_mode", c_int),
+    ]
+
+
 class TtsLaunchRecord(Structure):
     _fields_ = [("name", c_char * 48), ("flops", c_double), ("bytes", c_double), ("ms", c_float)]
 
@@ -180,11 +193,11 @@ SIGNATURES = {
     ),
     "tts_glow_decoder_destroy": (c_int, [c_void_p]),
     "tts_glow_decoder_forward": (
-        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]
     ),
     "tts_glow_decoder_forward_profiled": (
         c_int,
-        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_glow_encoder_num_weights": (c_int, [POINTER(TtsGlowEncoderCfg)]),
@@ -226,6 +239,19 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_posterior_num_weights": (c_int, [POINTER(TtsVitsPosteriorCfg)]),
+    "tts_vits_posterior_weight_numel": (c_int64, [POINTER(TtsVitsPosteriorCfg), c_int]),
+    "tts_vits_posterior_create": (c_int, [POINTER(TtsVitsPosteriorCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
+    "tts_vits_posterior_destroy": (c_int, [c_void_p]),
+    "tts_vits_posterior_forward": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                c_void_p]
+    ),
+    "tts_vits_posterior_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+         c_void_p, POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_op_conv1d": (
         c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]

@@ -62,6 +62,16 @@ VITS_FLOW: Dict[str, Any] = {
     "num_flows": 4,
 }
 
+# PosteriorEncoder of VitsArgs (vits.py:594-602): the linear spectrogram (fft_size 1024 -> 513 bins)
+VITS_POSTERIOR: Dict[str, Any] = {
+    "in_channels": 513,         # out_channels (fft_size // 2 + 1)
+    "out_channels": 192,        # hidden_channels
+    "hidden_channels": 192,
+    "kernel_size": 5,           # kernel_size_posterior_encoder
+    "dilation_rate": 1,         # dilation_rate_posterior_encoder
+    "num_layers": 16,           # num_layers_posterior_encoder
+}
+
 VITS_DECODER: Dict[str, Any] = {
     "in_channels": 192,
     "out_channels": 1,

@@ -178,6 +178,47 @@ def glow_decoder_state_dict(
     return sd
 
 
+def vits_posterior_state_dict(
+    in_channels: int = 513,
+    out_channels: int = 192,
+    hidden_channels: int = 192,
+    kernel_size: int = 5,
+    dilation_rate: int = 1,
+    num_layers: int = 16,
+    cond_channels: int = 0,
+    seed: int = 1357,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a VITS ``PosteriorEncoder`` (TTS/tts/layers/vits/networks.py:235-288) with
+    synthetic variance-preserving weights, in the reference's key order (pre, enc = WN with weight
+    norm, proj).  proj is scaled down so that exp(log_scale) stays O(1)."""
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    H = hidden_channels
+
+    def conv(name: str, cout: int, cin: int, k: int, scale: float):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        sd[f"{name}.weight"] = torch.from_numpy(w.astype(np.float32))
+        sd[f"{name}.bias"] = torch.from_numpy((rng.standard_normal((cout,)) * 0.02).astype(np.float32))
+
+    def wn_conv(name: str, cout: int, cin: int, k: int, scale: float):
+        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+        sd[f"{name}.bias"] = torch.from_numpy((rng.standard_normal((cout,)) * 0.02).astype(np.float32))
+        g, v = _wn_pair(rng, w)
+        sd[f"{name}.parametrizations.weight.original0"] = torch.from_numpy(g)
+        sd[f"{name}.parametrizations.weight.original1"] = torch.from_numpy(v)
+
+    conv("pre", H, in_channels, 1, 1.0)
+    for l in range(num_layers):
+        wn_conv(f"enc.in_layers.{l}", 2 * H, H, kernel_size, 1.0)
+    for l in range(num_layers):
+        wn_conv(f"enc.res_skip_layers.{l}", 2 * H if l < num_layers - 1 else H, H, 1, 1.0)
+    if cond_channels > 0:
+        wn_conv("enc.cond_layer", 2 * H * num_layers, cond_channels, 1, 0.5)
+    conv("proj", 2 * out_channels, H, 1, 0.3)
+    return sd
+
+
 def vits_flow_state_dict(
     channels: int = VITS_FLOW["channels"],
     hidden_channels: int = VITS_FLOW["hidden_channels"],

@@ -189,7 +189,7 @@ class Decoder(nn.Module):
         ws: List[np.ndarray] = []
         for b in range(self.num_flow_blocks):
             an, ic, cb = self.flows[3 * b], self.flows[3 * b + 1], self.flows[3 * b + 2]
-            ws += [_t(an.logs).reshape(-1), _t(an.bias).reshape(-1), _t(ic.inverse_weight())]
+            ws += [_t(an.logs).reshape(-1), _t(an.bias).reshape(-1), _t(ic.inverse_weight()), _t(ic.weight)]
             ws += [_w(cb.start), _t(cb.start.bias)]
             if self.c_in_channels > 0:
                 ws += [_w(cb.wn.cond_layer).reshape(-1), _t(cb.wn.cond_layer.bias)]
@@ -258,8 +258,8 @@ class Decoder(nn.Module):
         return g
 
     def forward(self, x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None, reverse: bool = False):
-        if not reverse:
-            raise NotImplementedError("tts_amd Decoder implements the reverse (inference) flow only")
+        """decoder.py:113-137: (y, None) for reverse=True (inference), (z, logdet [B]) for reverse=False
+        (GlowTTS.decoder_inference's first pass, glow_tts.py:333)."""
         with torch.no_grad():
             h = self._native_handle()
             dev = self._device()
@@ -271,12 +271,13 @@ class Decoder(nn.Module):
             gv = self._speaker(g, B, dev)
             Tq = (T // self.num_squeeze) * self.num_squeeze if self.num_squeeze > 1 else T
             y = torch.empty(B, C, Tq, device=dev, dtype=torch.float32)
-            N.call("tts_glow_decoder_forward", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1, N.ptr(y),
-                   N.stream_ptr(dev))
-        return y, None
+            logdet = None if reverse else torch.empty(B, device=dev, dtype=torch.float32)
+            N.call("tts_glow_decoder_forward", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1 if reverse else 0,
+                   N.ptr(y), N.ptr(logdet), N.stream_ptr(dev))
+        return y, logdet
 
-    def profile(self, x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None):
-        """One reverse pass with a hipEvent pair around every launch: (y, [{name, flops, bytes, ms}])."""
+    def profile(self, x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None, reverse: bool = True):
+        """One pass with a hipEvent pair around every launch: (y, [{name, flops, bytes, ms}])."""
         h = self._native_handle()
         dev = self._device()
         x = x.to(device=dev, dtype=torch.float32).contiguous()
@@ -285,11 +286,12 @@ class Decoder(nn.Module):
         gv = self._speaker(g, B, dev)
         Tq = (T // self.num_squeeze) * self.num_squeeze if self.num_squeeze > 1 else T
         y = torch.empty(B, C, Tq, device=dev)
+        logdet = None if reverse else torch.empty(B, device=dev, dtype=torch.float32)
         cap = 2048
         recs = (N.TtsLaunchRecord * cap)()
         n = ctypes.c_int(0)
-        N.call("tts_glow_decoder_forward_profiled", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1, N.ptr(y),
-               N.stream_ptr(dev), recs, cap, ctypes.byref(n))
+        N.call("tts_glow_decoder_forward_profiled", h, N.ptr(x), N.ptr(m), N.ptr(gv), B, C, T, 1 if reverse else 0,
+               N.ptr(y), N.ptr(logdet), N.stream_ptr(dev), recs, cap, ctypes.byref(n))
         rows = [{"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
                 for i in range(min(n.value, cap))]
         return y, rows

@@ -466,6 +466,25 @@ class GlowTTS(nn.Module):
             "total_durations_log": o_attn_dur.transpose(1, 2),
         }
 
+    @torch.no_grad()
+    def decoder_inference(self, y, y_lengths=None, aux_input={"d_vectors": None, "speaker_ids": None}):  # noqa: B006
+        """glow_tts.py:319-339: the decoder forward (mel -> z, reverse=False) then reverse (z -> mel),
+        y: [B, T, C] mel frames, y_lengths: [B].  Returns {"model_outputs": [B, T', C], "logdet": None}
+        (the reverse pass's logdet, as the reference's)."""
+        dev = self._device()
+        y = y.to(device=dev, dtype=torch.float32).transpose(1, 2)
+        B, _, T = y.shape
+        g = self._speaker_embedding(aux_input)
+        if self.c_in_channels and g is None:
+            raise ValueError("multi-speaker Glow-TTS: pass aux_input speaker_ids or d_vectors")
+        if y_lengths is None:
+            y_lengths = torch.full((B,), T, device=dev)
+        lens = torch.as_tensor(y_lengths, device=dev).reshape(B)
+        y_mask = (torch.arange(T, device=dev)[None, :] < lens[:, None]).to(torch.float32).unsqueeze(1)  # :331
+        z, logdet = self.decoder(y, y_mask, g=g, reverse=False)  # :333
+        y, logdet = self.decoder(z, y_mask[:, :, : z.shape[2]], g=g, reverse=True)  # :335
+        return {"model_outputs": y.transpose(1, 2), "logdet": logdet}
+
     def store_inverse(self):  # glow_tts.py:519-520
         self.decoder.store_inverse()
 
