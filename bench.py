@@ -91,6 +91,8 @@ def parse():
                    help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
     p.add_argument("--cpu-utts", type=int, default=0,
                    help="utterances of the bench batch the CPU baseline vocodes (0: the whole batch)")
+    p.add_argument("--vits-batch", type=int, default=64, help="config 5 global batch (N > 1 leg)")
+    p.add_argument("--vits-frames", type=int, default=1024, help="config 5 latent frames per utterance")
     p.add_argument("--comm-timeout", type=float, default=300.0, help="collective timeout (s), fail-fast")
     p.add_argument("--rank-timeout", type=float, default=1500.0,
                    help="a rank that runs longer than this dumps its stack and exits (hung peer)")
@@ -484,6 +486,96 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
     return out
 
 
+class StubVits:
+    """TEST ONLY (--stub): CPU stand-in of the VITS flow + decoder with the real output shape
+    (z [B, 192, T] -> wav [B, 1, 256 T])."""
+
+    def __call__(self, zp, mask, g):
+        return torch.tanh(zp.mean(1, keepdim=True) * mask + g.mean(1, keepdim=True)).repeat_interleave(256, dim=2)
+
+
+def vits_sharded_bench(dev, world, rank, steps, warmup, stub=False, global_batch=64, T=1024, cond=256,
+                       mode="bf16"):
+    """Config 5 (BASELINE.json configs[4]): VITS flow + 512-channel decoder, global batch 64 over the
+    ranks (strong scaling: 64 / world utterances each).  Rank 0 holds the [64, 192, T] latents, the
+    masks and the speaker vectors in HBM; one step scatters the three (RCCL), every rank runs
+    ResidualCouplingBlocks(reverse=True) -> z * mask -> the decoder on its shard, and rank 0 gathers
+    the waveforms.  Also reports the compute-only step and the collectives alone."""
+    from tts_amd import synthetic
+    from tts_amd.config import VITS_DECODER, VITS_FLOW
+    from tts_amd.sharding import gather_batch, scatter_batch, shard_sizes
+
+    n = global_batch
+    per = shard_sizes(n, world)[rank]
+    gen = torch.Generator().manual_seed(9)
+    full_z = full_m = full_g = None
+    if rank == 0:
+        full_z = torch.randn(n, 192, T, generator=gen).to(dev)
+        lens = torch.randint(T // 2, T + 1, (n,), generator=gen)
+        lens[0] = T
+        full_m = (torch.arange(T)[None] < lens[:, None]).float().unsqueeze(1).to(dev)
+        full_g = torch.randn(n, cond, 1, generator=gen).to(dev)
+    cap = max(shard_sizes(n, world))
+    bz = torch.empty(cap, 192, T, device=dev)
+    bm = torch.empty(cap, 1, T, device=dev)
+    bg = torch.empty(cap, cond, 1, device=dev)
+    if stub:
+        step_fn = StubVits()
+    else:
+        from tts_amd.tts import ResidualCouplingBlocks
+        from tts_amd.vocoder import HifiganGenerator
+
+        fcfg = dict(VITS_FLOW, cond_channels=cond)
+        dcfg = dict(VITS_DECODER, cond_channels=cond)
+        flow = ResidualCouplingBlocks(fcfg["channels"], fcfg["hidden_channels"], fcfg["kernel_size"],
+                                      fcfg["dilation_rate"], fcfg["num_layers"], num_flows=fcfg["num_flows"],
+                                      cond_channels=cond, math_mode=mode)
+        flow.load_state_dict(synthetic.vits_flow_state_dict(**fcfg, seed=2469))
+        flow = flow.to(dev)
+        dec = HifiganGenerator(**dcfg, math_mode=mode)
+        with contextlib.redirect_stdout(sys.stderr):
+            dec.remove_weight_norm()
+        dec.load_state_dict(synthetic.hifigan_state_dict(**dcfg, seed=99, weight_norm=False))
+        dec = dec.to(dev)
+
+        def step_fn(zp, mask, g):
+            return dec(flow(zp, mask, g=g, reverse=True) * mask, g=g)
+    S = 256 * T
+    wav_full = torch.empty(n, 1, S, device=dev) if rank == 0 else None
+
+    def scatter():
+        return (scatter_batch(full_z, n, (192, T), dev, out=bz), scatter_batch(full_m, n, (1, T), dev, out=bm),
+                scatter_batch(full_g, n, (cond, 1), dev, out=bg))
+
+    z, m, g = scatter()
+    z, m, g = z.clone(), m.clone(), g.clone()  # resident shard for the compute-only timing
+    wav = step_fn(z, m, g)
+
+    def step():
+        zs, ms, gs = scatter()
+        gather_batch(step_fn(zs, ms, gs), n, out=wav_full)
+
+    ms = timed(step, steps, warmup, dev, world)
+    compute_ms = timed(lambda: step_fn(z, m, g), steps, warmup, dev, world)
+    scatter_ms = timed(scatter, max(3, steps), 1, dev, world)
+    gather_ms = timed(lambda: gather_batch(wav, n, out=wav_full), max(3, steps), 1, dev, world)
+    step()
+    check = None
+    if rank == 0:  # rank 0's own rows, vocoded alone, equal the gathered ones bit for bit
+        check = bool(torch.equal(wav_full[:per], step_fn(full_z[:per], full_m[:per], full_g[:per])))
+    samples = n * S
+    return {
+        "workload": f"config 5: VITS flow reverse (4 flows, speaker cond {cond}) + 512-ch HiFiGAN decoder, global "
+                    f"batch {n} x {T} latent frames over {world} rank(s) ({per} each), rank 0 scatters latents / "
+                    f"masks / speaker vectors and gathers the waveforms (RCCL)",
+        "math_mode": "stub" if stub else mode, "scaling": "strong", "world_size": world, "global_batch": n,
+        "per_rank_batch": per, "ms_per_step": ms, "samples_per_s": samples / (ms / 1e3),
+        "rtf": (ms / 1e3) / (samples / SAMPLE_RATE),
+        "compute_only_ms_per_step": compute_ms, "scatter_ms": scatter_ms, "gather_ms": gather_ms,
+        "rank0_rows_bitwise_equal": check,
+    }
+
+
 def rank_devices(world, rank, local, dev):
     """Every rank's (rank, local rank, device, PCI bus) as torch.distributed saw it."""
     me = {"rank": rank, "local_rank": local, "device": str(dev)}
@@ -611,6 +703,11 @@ def main():
             "utterances": shard["utterances"], "mel_bytes": shard["mel_bytes"], "wav_bytes": shard["wav_bytes"],
             "last_shard_bitwise_equal": shard["last_shard_bitwise_equal"],
         }
+    if world > 1 and not a.no_vits:  # config 5 at N > 1 (its N = 1 side line is vits_waveform)
+        v5 = vits_sharded_bench(dev, world, rank, a.steps, a.warmup, stub=a.stub, global_batch=a.vits_batch,
+                                T=a.vits_frames)
+        if rank == 0:
+            rec["config5_sharded"] = v5
     if a.stub:
         rec["data"] = "STUB (test only): CPU stand-in vocoder, not a measurement"
         rec["dtype"] = "fp32"

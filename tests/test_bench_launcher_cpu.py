@@ -31,7 +31,8 @@ def _json_line(stdout: str) -> dict:
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_launches_n_ranks_and_reports_world(world):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--stub", "--steps", "2", "--warmup", "1",
-                        "--batch", "3", "--frames", "12"], env=_env(), capture_output=True, text=True, timeout=300)
+                        "--batch", "3", "--frames", "12", "--vits-batch", "7", "--vits-frames", "10"], env=_env(),
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == world and rec["world_size"] == world
@@ -45,6 +46,14 @@ def test_bench_launches_n_ranks_and_reports_world(world):
     # value = all ranks' samples / the max-over-ranks step time
     samples = 3 * world * 256 * (12 + 10)
     assert rec["value"] == pytest.approx(samples / (rec["ms_per_step"] / 1e3), rel=1e-9)
+    # config 5 at N > 1: global batch 7 split over the ranks (strong scaling), scatter/gather of
+    # latents, masks and speaker vectors, rank 0's gathered rows equal its shard vocoded alone
+    v5 = rec["config5_sharded"]
+    assert v5["world_size"] == world and v5["global_batch"] == 7 and v5["scaling"] == "strong"
+    assert v5["per_rank_batch"] == -(-7 // world)
+    assert v5["rank0_rows_bitwise_equal"] is True
+    assert v5["scatter_ms"] > 0 and v5["gather_ms"] > 0 and v5["compute_only_ms_per_step"] > 0
+    assert v5["samples_per_s"] == pytest.approx(7 * 256 * 10 / (v5["ms_per_step"] / 1e3), rel=1e-9)
 
 
 def test_bench_single_rank_has_no_collectives():
@@ -52,7 +61,7 @@ def test_bench_single_rank_has_no_collectives():
                         "--frames", "8"], env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
-    assert rec["n_gpus"] == 1 and "sharded" not in rec
+    assert rec["n_gpus"] == 1 and "sharded" not in rec and "config5_sharded" not in rec
 
 
 def test_bench_refuses_world_size_mismatch():

@@ -404,6 +404,10 @@ constexpr int R3_LEAD = 12;
 // GEO 3: 128 columns, 8 waves (4 row blocks x 2 column halves at C = 128, two waves per SIMD).
 // Measured (f16x3, per batch): C = 128 GEO 3 5.0 ms vs GEO 2 5.5 ms; 8-wave forms at C = 64
 // (256 columns) and C = 32 (512 columns) were slower than GEO 2 / GEO 0 (+0.2 / +0.3 ms).
+#ifndef RES3_LATE_XR
+#define RES3_LATE_XR 1  // whole-block kernel: the acc-layout residual read after the window landed
+#endif
+
 template <class S, int C, int GEO>
 struct Res3Cfg {
   static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
@@ -484,18 +488,24 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) xv[g][i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
       }
+    // x0 in the acc layout (the residual): the same bytes as the window, so read once the window
+    // has landed (L2 hits; issued together, both missed L2: 2.4x the x plane in FETCH_SIZE).  It is
+    // first needed in conv 1's epilogue, so its latency hides behind conv 1's MFMAs.
+    auto load_xr = [&] {
 #pragma unroll
-    for (int m = 0; m < TM; ++m)
+      for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int t = tx0 + xcol0 + n * 32;
-        const bool tok = t >= 0 && t < T;
+        for (int n = 0; n < TN; ++n) {
+          const int t = tx0 + xcol0 + n * 32;
+          const bool tok = t >= 0 && t < T;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+          for (int r = 0; r < 16; ++r) {
+            const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+          }
         }
-      }
+    };
+    if (!RES3_LATE_XR) load_xr();
 #pragma unroll
     for (int g = 0; g < NC; ++g)
 #pragma unroll
@@ -513,6 +523,10 @@ void resblock3_kernel(ResBlock3Args a) {
           split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * q, v[0], v[1], v[2], v[3]);
         }
       }
+    if (RES3_LATE_XR) {
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads below the window's use
+      load_xr();
+    }
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
