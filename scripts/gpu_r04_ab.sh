@@ -11,9 +11,10 @@ if [ -z "$AB_SKIP_TESTS" ]; then
   tail -1 gpurun_out/ab_pytest.log
 fi
 B="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits"
+VARS=${AB_VARIANTS:-base new}
 for r in 1 2; do
-  for v in base new; do
-    lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so; [ $v = base ] && lib=ab/lib_base.so
+  for v in $VARS; do
+    lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so; [ $v != new ] && lib=ab/lib_$v.so
     TTS_MI355X_LIB=$lib timeout -k 10 200 python $B > gpurun_out/ab_${v}_$r.json 2> gpurun_out/ab_${v}_$r.err || { tail -5 gpurun_out/ab_${v}_$r.err; exit 1; }
     python -c "
 import json,re;d=json.load(open('gpurun_out/ab_${v}_$r.json'));b=d['kernel_breakdown_ms']
@@ -22,8 +23,8 @@ print('${v}_$r', round(d['ms_per_step'],2), {k: round(v,2) for k,v in b.items() 
 done
 [ -n "$NO_PMC" ] && exit 0
 P="bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits"
-for v in base new; do
-  lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so; [ $v = base ] && lib=ab/lib_base.so
+for v in ${PMC_VARIANTS:-$VARS}; do
+  lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so; [ $v != new ] && lib=ab/lib_$v.so
   OUT=gpurun_out/pmc_$v; mkdir -p $OUT
   export TTS_FORWARD_NAMES=$OUT/forward_names.json
   TTS_MI355X_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/p1 -o p1 --output-format csv -- python3 $P > $OUT/p1.log 2>&1 || { echo "pmc $v failed"; tail -5 $OUT/p1.log; exit 1; }

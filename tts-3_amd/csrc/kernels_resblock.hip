@@ -404,10 +404,6 @@ constexpr int R3_LEAD = 12;
 // GEO 3: 128 columns, 8 waves (4 row blocks x 2 column halves at C = 128, two waves per SIMD).
 // Measured (f16x3, per batch): C = 128 GEO 3 5.0 ms vs GEO 2 5.5 ms; 8-wave forms at C = 64
 // (256 columns) and C = 32 (512 columns) were slower than GEO 2 / GEO 0 (+0.2 / +0.3 ms).
-#ifndef RES3_LATE_XR
-#define RES3_LATE_XR 1  // whole-block kernel: the acc-layout residual read after the window landed
-#endif
-
 template <class S, int C, int GEO>
 struct Res3Cfg {
   static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
@@ -505,7 +501,6 @@ void resblock3_kernel(ResBlock3Args a) {
           }
         }
     };
-    if (!RES3_LATE_XR) load_xr();
 #pragma unroll
     for (int g = 0; g < NC; ++g)
 #pragma unroll
@@ -523,10 +518,8 @@ void resblock3_kernel(ResBlock3Args a) {
           split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * q, v[0], v[1], v[2], v[3]);
         }
       }
-    if (RES3_LATE_XR) {
-      __builtin_amdgcn_sched_barrier(0);  // keep the loads below the window's use
-      load_xr();
-    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads below the window's use
+    load_xr();
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll

@@ -40,10 +40,6 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
     }                                                                                                        \
   } while (0)
 
-#ifndef WINO8_DEINT
-#define WINO8_DEINT 1  // D > 1: residue-de-interleaved raw window by dword LDS-DMA (0: the D = 1 layout)
-#endif
-
 template <class S, int K, int D>
 struct Wino8Cfg {
   static constexpr int NCH = wino_chunks(K);
@@ -61,17 +57,8 @@ struct Wino8Cfg {
   static constexpr int RSPAN4 = (RSPAN + 3) / 4 * 4;
   static constexpr int RPITCH = RSPAN4 % 8 == 4 ? RSPAN4 : RSPAN4 + 4;  // RPITCH / 4 odd
   static constexpr int RF4 = (16 * RPITCH / 4 + 63) / 64 * 64;          // float4s per raw buffer (DMA rows of 64)
-  // D > 1 (DEINT): row (ch, rho) of the raw buffer holds x[t0 - PAD + rho + D i], i < 4 RP, so a
-  // column's 7 inputs are 7 consecutive floats of one row (two aligned ds_read_b128) instead of 7
-  // ds_read_b32 D apart (2- to 4-way bank conflicts).  Rows RP float4s apart, channels CP = D RP;
-  // RP from an exhaustive bank model of the job reads (scripts/wino_banks.py): conflict-free.
-  static constexpr bool DEINT = WINO8_DEINT && D > 1;
-  static constexpr int RP = D == 3 ? 27 : 17;
-  static constexpr int CP = D * RP;
-  static constexpr int NDW = (16 * CP * 4 + 63) / 64;  // dword DMA instructions per chunk
-  static constexpr int RSZ = DEINT ? NDW * 256 : RF4 * 16;
-  static constexpr int NDMA = DEINT ? NDW : RF4 / 64;  // DMA instructions per chunk (waves 4-7)
-  static_assert(!DEINT || 4 * RP >= 4 * ((XROWS - 1) / D) + 7, "residue row shorter than its columns' inputs");
+  static constexpr int RSZ = RF4 * 16;
+  static constexpr int NDMA = RF4 / 64;              // DMA instructions per chunk (waves 4-7)
   static constexpr int UNITS = XROWS * 4;            // (column, channel quad)
   static constexpr int UPW = (UNITS + 7) / 8;        // units per wave
   static constexpr int PITCH = 256;                  // epilogue transpose row (samples)
@@ -123,34 +110,17 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const unsigned chb = (unsigned)Tin * 4u;
 
   // ---- input DMA (waves 4-7): raw[ch][RPITCH] fp32, window start ta = t0 - PAD - ROFF ----
-  const int ta = C::DEINT ? t0 - C::PAD : t0 - C::PAD - C::ROFF;
+  const int ta = t0 - C::PAD - C::ROFF;
   // DMA instructions i = wm + 4k of raw(c) -> R[rb], for k in [k0, k1) (wave-uniform)
   auto dma = [&](int c, int rb, int k0 = 0, int k1 = 64) {
     const int c0 = c * 16;
     const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
     for (int i = wm + 4 * k0; i < C::NDMA && i < wm + 4 * k1; i += 4) {
-      if constexpr (C::DEINT) {
-        // dword e = 64 i + lane of the buffer: channel e / (4 CP), residue row, element; the
-        // instruction's first dword is wave-uniform, so only one channel step can occur per lane
-        const int e0 = i * 64;
-        const int ch0 = e0 / (4 * C::CP);
-        int r = e0 - ch0 * (4 * C::CP) + lane;
-        int ch = ch0;
-        if (r >= 4 * C::CP) { r -= 4 * C::CP; ++ch; }
-        int rho = 0;
-#pragma unroll
-        for (int q = 1; q < D; ++q) rho += r >= q * 4 * C::RP ? 1 : 0;
-        const int t = ta + rho + D * (r - rho * 4 * C::RP);
-        const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 256), 4, (int)vo, 0, 0, 0);
-      } else {
-        const int f = i * 64 + lane;
-        const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
-        const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
-      }
+      const int f = i * 64 + lane;
+      const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
+      const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
     }
   };
 
@@ -167,9 +137,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // each lane of waves 4-7 takes one (unit, piece pair) job, dealt round-robin over the four waves,
   // so every SIMD runs the transform instructions of one full and one half pass; otherwise wave 4
   // alone takes them whole and its SIMD runs two full passes per chunk while the others run one.
-  const int e = lane * 4 + (wave - 4);  // leftover job of a waves-4-7 lane
-  const int u = WINO8_DENSE ? (grp == 0 ? wave * 64 + lane
-                                        : (WINO8_SPREAD ? 256 + (e >> 1) : (wave == 4 ? 256 + lane : C::UNITS)))
+  constexpr int TG = 0;  // the point group whose waves take the dense units (the DMA waves: slower)
+  const int e = lane * 4 + wm;  // leftover job of a lane of the other group
+  const int u = WINO8_DENSE ? (grp == TG ? wm * 64 + lane
+                                         : (WINO8_SPREAD ? 256 + (e >> 1) : (wm == 0 ? 256 + lane : C::UNITS)))
                             : wave * C::UPW + lane;
   const bool uok = (WINO8_DENSE || lane < C::UPW) && u < C::UNITS;
   // pieces a lane transforms: all four, or one pair (2 jp, 2 jp + 1) for a spread leftover job
@@ -183,26 +154,21 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // aligned float4s (ds_read_b128).  The lanes of a 16-lane group hold 4 columns x 4 channel quads:
   // float4 slots c * RPITCH / 4 + urow, RPITCH / 4 odd, cover all 16 slots of the bank row (no
   // conflict), where 7 ds_read_b32 at one sub-offset put 32 lanes on 8 banks (4-way)
-  constexpr int NU = C::DEINT ? 2 : (C::ROFF + 6) / 4 + 1;
+  constexpr int NU = (C::ROFF + 6) / 4 + 1;
   f32x4 jraw4[NU];
   // piece j: channel 4q + j; pairs are written after channels 1 and 3.  A piece runs in two parts
   // one MFMA step apart: job_load issues its 7 LDS reads, job_finish transforms (and splits and
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
   // job index j = 0..3 -> channel piece (a spread lane maps its jobs 0, 1 onto its pair; 2, 3 are empty)
-  auto piece = [&](int j) { return SPREAD && grp == 1 ? 2 * jp + j : j; };
+  auto piece = [&](int j) { return SPREAD && grp != TG ? 2 * jp + j : j; };
   auto job_load = [&](int rb, int j) {
-    if (SPREAD && grp == 1 && j >= 2) return;
+    if (SPREAD && grp != TG && j >= 2) return;
     if (!uok) return;
     if constexpr (D == 1) {
       const f32x4* raw4 =
           reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * (C::RPITCH / 4) + urow;
 #pragma unroll
       for (int u4 = 0; u4 < NU; ++u4) jraw4[u4] = raw4[u4];
-    } else if constexpr (C::DEINT) {
-      const f32x4* raw4 = reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::CP +
-                          urho * C::RP + ujj;
-      jraw4[0] = raw4[0];
-      jraw4[1] = raw4[1];
     } else {
       const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::RPITCH + uri;
 #pragma unroll
@@ -210,12 +176,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     }
   };
   auto job_finish = [&](int tb, int j) {
-    if (SPREAD && grp == 1 && j >= 2) return;
+    if (SPREAD && grp != TG && j >= 2) return;
     if (!uok) return;
     float v[7], t[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      float x = D == 1 ? jraw4[(C::ROFF + k) / 4][(C::ROFF + k) % 4] : (C::DEINT ? jraw4[k / 4][k % 4] : jraw[k]);
+      float x = D == 1 ? jraw4[(C::ROFF + k) / 4][(C::ROFF + k) % 4] : jraw[k];
       if (LRELU) x = lrelu2(x, slope);
       v[k] = H3 ? x * xscale : x;
     }
@@ -290,17 +256,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
     // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
     // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
-    // (DEINT k7: distance 4 for the DMA waves, whose per-step dword DMA address math needs the
-    // registers; 6 spills)
-    constexpr int PD = P0 > 0 ? (C::DEINT && K == 7 ? 4 : WINO8_PD1) : WINO8_PD;
+    constexpr int PD = P0 > 0 ? WINO8_PD1 : WINO8_PD;
     // steps between a transform piece's LDS reads and its math (no later than the next piece's
     // reads); measured per kernel size
-    constexpr int NPW = (C::NDMA + 3) / 4;                    // DMA instructions per wave and chunk (max)
-    constexpr int DPS = (NPW + NV - 2) / (NV - 1 > 0 ? NV - 1 : 1);  // DEINT: per step, steps 0 .. NV-2
-    constexpr int VLAST = C::DEINT ? (NPW + DPS - 1) / DPS - 1 : 2;  // the last step that issues DMA
-    static_assert(!C::DEINT || VLAST <= NV - 1, "");
-    // (DEINT k7: the one-step gap keeps two float4s per lane live across a step: spills)
-    constexpr int GAP0 = K == 11 ? WINO8_GAP11 : (C::DEINT ? 0 : WINO8_GAP7);
+    constexpr int GAP0 = K == 11 ? WINO8_GAP11 : WINO8_GAP7;
     constexpr int GAP = GAP0 < NV / 4 ? GAP0 : NV / 4;
     auto aoff = [&](int ck, int v) {  // byte soffset of virtual step v of chunk ck (v may run past NV)
       const int ck2 = ck + v / NV, v2 = v % NV;
@@ -332,15 +291,8 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) ar[PD][q] = bload4(ra, avoff, aoff(ck, v + PD) + (unsigned)q * 1024u);
         if (v + 1 < NV) read_b(tl, v + 1, bnext);
-        // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed): two DMA instructions per step over steps 0-2,
-        // or (DEINT, ~21 dword instructions per wave) DPS per step over steps 0 .. NV-2
-        if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc) {
-          if constexpr (C::DEINT) {
-            if (v * DPS < NPW) dma(ck + 2, tb, v * DPS, (v + 1) * DPS);
-          } else if (v < 3) {
-            dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);
-          }
-        }
+        // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed), two DMA instructions per step
+        if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc && v < 3) dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);
         __builtin_amdgcn_sched_barrier(0);
         const int p = v % NPG;
 #pragma unroll
@@ -376,7 +328,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       }
       // raw(ck+2) landed: at most the weight loads issued after the last DMA (steps 3.. of this chunk)
       // may still be in flight
-      constexpr int NAFTER = C::DEINT ? (NV - 1 - VLAST) * NP : (PD < NV - 3 ? PD : NV - 3) * NP;
+      constexpr int NAFTER = (PD < NV - 3 ? PD : NV - 3) * NP;
       if (P0 > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NAFTER) : "memory");
       if (ck < 8) WSTAMP(4 + 2 * ck);
       lds_sync();

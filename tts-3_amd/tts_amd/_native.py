@@ -341,7 +341,10 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(f"{LIB_PATH} implements C-ABI {abi}, these bindings need {ABI_VERSION}: "
                            "rebuild it with `make -C tts-3_amd`")
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(handle, name)
+        try:
+            fn = getattr(handle, name)
+        except AttributeError:  # a call to it raises the same error (tests check every symbol is exported)
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = handle
