@@ -20,6 +20,13 @@
 
 namespace tts {
 
+#ifndef XT_ABLATE
+#define XT_ABLATE 0  // timing-only builds (wrong results): 1 = conflict-free (misplaced) xt stores
+#endif
+// the 32 lanes of a half write rows l32 at one column position: dword 20 row + c, 8 banks (4-way);
+// the ablation adds (l32 >> 3) dwords so they cover 32 banks, to price the conflict
+#define XT_ABLATE_OFF (XT_ABLATE ? 4 * ((threadIdx.x & 31) >> 3) : 0)
+
 
 // Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
 // 32x32 blocks; RP_W = convs1 columns, RP_BN = RP_W - 2 * LEAD output columns.
@@ -258,7 +265,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
           const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
           unsigned w[NP];
           S::split2(acc[m][n][r] * tscale, acc[m][n][r + 1] * tscale, w);
-          unsigned char* dst = smem + ((co >> 4) * P::TROWS + row) * S::ROWB + 2 * (co & 15);
+          unsigned char* dst = smem + ((co >> 4) * P::TROWS + row) * S::ROWB + 2 * (co & 15) + XT_ABLATE_OFF;
 #pragma unroll
           for (int p = 0; p < NP; ++p)
             *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];
@@ -625,7 +632,7 @@ void resblock3_kernel(ResBlock3Args a) {
           const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
           unsigned w[NP];
           S::split2(acc[m][n][r] * scale, acc[m][n][r + 1] * scale, w);
-          unsigned char* dst = smem + ((co >> 4) * PR + row) * S::ROWB + 2 * (co & 15);
+          unsigned char* dst = smem + ((co >> 4) * PR + row) * S::ROWB + 2 * (co & 15) + XT_ABLATE_OFF;
 #pragma unroll
           for (int p = 0; p < NP; ++p)
             *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];

@@ -146,9 +146,6 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // pieces a lane transforms: all four, or one pair (2 jp, 2 jp + 1) for a spread leftover job
   constexpr bool SPREAD = WINO8_DENSE && WINO8_SPREAD;
   const int jp = e & 1;
-  const int urow = u >> 2, uq = u & 3;
-  const int ujj = urow / D, urho = urow - (urow / D) * D;
-  const int uri = urho + 4 * D * ujj + C::ROFF;  // raw index of the column's first input
   float tkeep[7], jraw[7];
   // D = 1: a column's 7 inputs are raw floats 4 urow + ROFF ... + 6 of its channel row, read as NU
   // aligned float4s (ds_read_b128).  The lanes of a 16-lane group hold 4 columns x 4 channel quads:
@@ -161,16 +158,19 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
   // job index j = 0..3 -> channel piece (a spread lane maps its jobs 0, 1 onto its pair; 2, 3 are empty)
   auto piece = [&](int j) { return SPREAD && grp != TG ? 2 * jp + j : j; };
+  const int jrow = u >> 2, jq = u & 3;  // the lane's unit: column row, channel quad
   auto job_load = [&](int rb, int j) {
     if (SPREAD && grp != TG && j >= 2) return;
     if (!uok) return;
     if constexpr (D == 1) {
       const f32x4* raw4 =
-          reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * (C::RPITCH / 4) + urow;
+          reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * (C::RPITCH / 4) + jrow;
 #pragma unroll
       for (int u4 = 0; u4 < NU; ++u4) jraw4[u4] = raw4[u4];
     } else {
-      const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * uq + piece(j)) * C::RPITCH + uri;
+      const int jjj = jrow / D, jrho = jrow - jjj * D;
+      const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * C::RPITCH +
+                         jrho + 4 * D * jjj + C::ROFF;
 #pragma unroll
       for (int k = 0; k < 7; ++k) jraw[k] = raw[D * k];
     }
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     }
     // word uq + 4 * pair of the row (channels 4 uq + 2 pair, +1; the weights are packed in this
     // channel order, pack_conv1d_wino): a 32-lane half (8 rows x 4 quads) covers all 32 banks
-    unsigned char* base = tsm + tb * C::TSZ + urow * S::ROWB + 4 * uq + 16 * (piece(j) >> 1);
+    unsigned char* base = tsm + tb * C::TSZ + jrow * S::ROWB + 4 * jq + 16 * (piece(j) >> 1);
 #pragma unroll
     for (int p = 0; p < kWinoPoints; ++p) {
       unsigned w[NP];
@@ -349,6 +349,8 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     if (sum == 1234.5f) a.y[threadIdx.x] = sum;
     return;
   }
+  // the f16x3 rescale sc (an exact power of two) commutes with the output transform: applied once
+  // per output in wino_apply instead of once per point here
   const float sc = H3 ? ldexpf(1.f, ex + a.w_exp) : 1.f;
   // partial outputs of this wave's points: yp[n][i][r]
   float yp[2][4][16];
@@ -357,14 +359,14 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (grp == 0) {
-        const float m0 = acc[0][n][r] * sc, m1 = acc[1][n][r] * sc, m2 = acc[2][n][r] * sc, m3 = acc[3][n][r] * sc;
+        const float m0 = acc[0][n][r], m1 = acc[1][n][r], m2 = acc[2][n][r], m3 = acc[3][n][r];
         const float s12 = m1 + m2, d12 = m1 - m2;
         yp[n][0][r] = (m0 + s12) + m3;
         yp[n][1][r] = fmaf(2.f, m3, d12);
         yp[n][2][r] = fmaf(4.f, m3, s12);
         yp[n][3][r] = fmaf(8.f, m3, d12);
       } else {
-        const float m4 = acc[0][n][r] * sc, m5 = acc[1][n][r] * sc, m6 = acc[2][n][r] * sc;
+        const float m4 = acc[0][n][r], m5 = acc[1][n][r], m6 = acc[2][n][r];
         yp[n][0][r] = m4 + m5;
         yp[n][1][r] = fmaf(-2.f, m4, 0.5f * m5);
         yp[n][2][r] = fmaf(4.f, m4, 0.25f * m5);
@@ -418,13 +420,17 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       const int t = t0 + 4 * (nk * 32 + l32);
       const int nvalid = Tout - t < 4 ? (Tout - t > 0 ? Tout - t : 0) : 4;
       const bool full = nvalid == 4 && (Tout & 3) == 0;
+      // gather GR vectors (residual, MRF sum) before computing and storing them: all 16 at once
+      // pay one memory latency per tile instead of two (the accumulators are dead by now); with
+      // both a residual and an MRF sum to read, 16 at once would spill, so two rounds of 8
+      constexpr int GR = (RES && ZM >= 2) ? 8 : 16;
 #pragma unroll
-      for (int r0 = 0; r0 < 16; r0 += 8) {  // gather 8 vectors, then compute and store them
-        float bias[8];
-        unsigned voff[8];
-        WinoIn gin[8];
+      for (int r0 = 0; r0 < 16; r0 += GR) {
+        float bias[GR];
+        unsigned voff[GR];
+        WinoIn gin[GR];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < GR; ++k) {
           const int r = r0 + k;
           const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
           bias[k] = wbias[co - (unsigned)(mt * 128)];
@@ -432,10 +438,10 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
           gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < GR; ++k) {
           const int r = r0 + k;
           const f32x4 yv = {y[0][r], y[1][r], y[2][r], y[3][r]};
-          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[k], oslope, zdiv, gin[k], nvalid, vmax);
+          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[k], oslope, zdiv, gin[k], nvalid, vmax, sc);
           wino_store(rout, v, voff[k], full, nvalid);
         }
       }
@@ -473,7 +479,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
           const f32x4 yv = *reinterpret_cast<const f32x4*>(tile + (grp * 8 + rr) * C::PITCH + tl);
-          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[rr], oslope, zdiv, gin[rr], nvalid, vmax);
+          const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[rr], oslope, zdiv, gin[rr], nvalid, vmax, sc);
           wino_store(rout, v, voff[rr], full, nvalid);
         }
         lds_sync();

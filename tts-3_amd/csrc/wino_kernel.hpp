@@ -126,11 +126,12 @@ __device__ __forceinline__ WinoIn wino_gather(const rsrc_t& rres, const rsrc_t& 
 
 template <bool RES, int ZM, bool H3>
 __device__ __forceinline__ f32x4 wino_apply(f32x4 y, float bias, float oslope, float zdiv, const WinoIn& g, int nvalid,
-                                             float& vm) {
+                                             float& vm, float sc = 1.f) {
   f32x4 v;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float x = lrelu2(y[j] + bias, oslope);
+    // sc: the f16x3 rescale (an exact power of two), so fma(y, sc, bias) rounds like (y * sc) + bias
+    float x = lrelu2(fmaf(y[j], sc, bias), oslope);
     if (RES) x = x + g.rv[j];
     if (ZM == 2) x = g.zv[j] + x;
     if (ZM == 3) x = (g.zv[j] + x) / zdiv;
