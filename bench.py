@@ -93,6 +93,9 @@ def parse():
                    help="utterances of the bench batch the CPU baseline vocodes (0: the whole batch)")
     p.add_argument("--vits-batch", type=int, default=64, help="config 5 global batch (N > 1 leg)")
     p.add_argument("--vits-frames", type=int, default=1024, help="config 5 latent frames per utterance")
+    p.add_argument("--rehearse-sharded", action="store_true",
+                   help="N = 1 only: run the config-4 / config-5 sharded legs over a one-rank process group "
+                        "(exercises the RCCL scatter/gather path on one GPU; reported under *_rehearsal)")
     p.add_argument("--comm-timeout", type=float, default=300.0, help="collective timeout (s), fail-fast")
     p.add_argument("--rank-timeout", type=float, default=1500.0,
                    help="a rank that runs longer than this dumps its stack and exits (hung peer)")
@@ -632,15 +635,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     faulthandler.dump_traceback_later(a.rank_timeout, exit=True)  # a hung peer ends this rank
+    rehearse = a.rehearse_sharded and world == 1
+    dist_on = world > 1 or rehearse
+    if rehearse:  # a one-rank process group (no torchrun needed)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     if a.stub:
         dev = torch.device("cpu")
-        if world > 1:
+        if dist_on:
             from tts_amd.sharding import init_distributed
             init_distributed("gloo", local, a.comm_timeout)
         g = StubVocoder()
     else:
         dev = torch.device("cuda", local)
-        if world > 1:
+        if dist_on:
             from tts_amd.sharding import init_distributed
             init_distributed("nccl", local, a.comm_timeout)
         g = build_generator(a.math_mode, dev)
@@ -656,11 +666,9 @@ def main():
     sync(dev)
     compute_ms = time_steps(g, mel, a.steps, a.warmup, dev, world)
     shard = None
-    if world > 1:
+    if dist_on:
         shard = sharded_step_bench(g, B, T, dev, world, rank, a.steps, a.warmup)
-        ms_per_step = shard["ms"]
-    else:
-        ms_per_step = compute_ms
+    ms_per_step = shard["ms"] if world > 1 else compute_ms
     value = world * samples_per_step / (ms_per_step / 1e3)
     rtf = (ms_per_step / 1e3) / (world * samples_per_step / SAMPLE_RATE)
 
@@ -695,7 +703,7 @@ def main():
         "devices": devices,
     }
     if shard is not None:
-        rec["sharded"] = {
+        rec["sharded_rehearsal" if rehearse else "sharded"] = {
             "compute_only_ms_per_step": compute_ms,
             "compute_only_value": world * samples_per_step / (compute_ms / 1e3),
             "scatter_ms": shard["scatter_ms"], "gather_ms": shard["gather_ms"],
@@ -703,17 +711,17 @@ def main():
             "utterances": shard["utterances"], "mel_bytes": shard["mel_bytes"], "wav_bytes": shard["wav_bytes"],
             "last_shard_bitwise_equal": shard["last_shard_bitwise_equal"],
         }
-    if world > 1 and not a.no_vits:  # config 5 at N > 1 (its N = 1 side line is vits_waveform)
+    if dist_on and not a.no_vits:  # config 5 at N > 1 (its N = 1 side line is vits_waveform)
         v5 = vits_sharded_bench(dev, world, rank, a.steps, a.warmup, stub=a.stub, global_batch=a.vits_batch,
                                 T=a.vits_frames)
         if rank == 0:
-            rec["config5_sharded"] = v5
+            rec["config5_sharded_rehearsal" if rehearse else "config5_sharded"] = v5
     if a.stub:
         rec["data"] = "STUB (test only): CPU stand-in vocoder, not a measurement"
         rec["dtype"] = "fp32"
         if rank == 0:
             print(json.dumps(rec), flush=True)
-        if world > 1:
+        if dist_on:
             dist.barrier()
             dist.destroy_process_group()
         return

@@ -14,3 +14,7 @@ unset TTS_ERRLOG
 [ -n "$NO_BENCH" ] && exit 0
 timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/bench.json'));print(d['ms_per_step'],d['value'],d['build']);print(d['roofline']);print(d['cpu_baseline'])"
+[ -n "$NO_REHEARSE" ] && exit 0
+# config-4 / config-5 sharded legs over a one-rank RCCL group (the N > 1 code path on one GPU)
+timeout -k 10 300 python3 -u bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline --no-glow --no-e2e --no-xtts --rehearse-sharded > gpurun_out/bench_rehearse.json 2> gpurun_out/bench_rehearse.err || { tail -20 gpurun_out/bench_rehearse.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/bench_rehearse.json'));print(d.get('sharded_rehearsal'));print(d.get('config5_sharded_rehearsal'))"

@@ -64,6 +64,22 @@ def test_bench_single_rank_has_no_collectives():
     assert rec["n_gpus"] == 1 and "sharded" not in rec and "config5_sharded" not in rec
 
 
+def test_bench_rehearse_sharded_single_rank():
+    """--rehearse-sharded at N = 1: both sharded legs over a one-rank group, reported beside (not
+    instead of) the headline value."""
+    r = subprocess.run([sys.executable, BENCH, "--stub", "--rehearse-sharded", "--steps", "2", "--warmup", "0",
+                        "--batch", "2", "--frames", "8", "--vits-batch", "3", "--vits-frames", "6"],
+                       env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 1 and "sharded" not in rec and "config5_sharded" not in rec
+    assert rec["sharded_rehearsal"]["last_shard_bitwise_equal"] is True
+    v5 = rec["config5_sharded_rehearsal"]
+    assert v5["world_size"] == 1 and v5["per_rank_batch"] == 3 and v5["rank0_rows_bitwise_equal"] is True
+    # the headline stays the compute-only step at N = 1
+    assert rec["value"] == pytest.approx(2 * 256 * (8 + 10) / (rec["ms_per_step"] / 1e3), rel=1e-9)
+
+
 def test_bench_refuses_world_size_mismatch():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--stub", "--steps", "1"],
                        env=_env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
