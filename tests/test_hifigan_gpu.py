@@ -162,6 +162,9 @@ CONVT_CASES = [
     (3, 40, 20, 9, 8),    # ragged
     (2, 128, 64, 70, 8),  # window-resident x8 form at 128 input channels (2 passes of 256 rows)
     (3, 256, 128, 129, 8),  # window-resident x8 form: frames across two 64-frame tiles + the pad frame
+    (2, 512, 256, 130, 8),  # x8, 512 channels: 3 windows, each window's 8 passes over 4 workgroups
+    (1, 256, 128, 260, 8),  # x8, 256 channels: windows across a 128-frame boundary too
+    (2, 64, 32, 513, 2),    # x2 window form, 64 channels: 514 frames over 128-frame windows
 ]
 
 

@@ -206,7 +206,15 @@ void pack_convT(const float* w, int Cin, int Cout, int U, const ConvTile& t, flo
 int64_t packed_convT_numel(int Cin, int Cout, int U, const ConvTile& t);
 // Split modes: [mblock32][cgroup16][K][piece][64][8 x 16-bit] (+4 steps of slack).  Returns the
 // exponent e with which the weights were pre-scaled by 2^-e (0 for bf16x6).
-int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out);
+// Channel order of the split kernels' 16-channel LDS rows and packed weights: the 16-bit position
+// of channel quad q is 4 quad_pos(q) (quads 1 and 2 swapped).  A wave's accumulator layout then
+// holds, per lane and 16-channel group, the 8 channels of 8 consecutive positions (8 half .. +7:
+// channels (r & 3) + 8 ((r >> 2) & 1) + 4 half), so an output tile handed to the next conv through
+// LDS is one 16-byte store per piece (conflict-free) instead of eight 32-bit ones (4-way).
+__host__ __device__ constexpr int quad_pos(int q) { return q == 1 ? 2 : (q == 2 ? 1 : q); }
+// quad_perm = false: position = channel (the Winograd packer applies its own order)
+int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out,
+                      bool quad_perm = true);
 int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const ConvTile& t);
 // ConvTranspose1d torch weight [Cin][Cout][2U] as the K=2 conv of Conv1dArgs::ups (U*Cout rows);
 // returns w_exp.  Its bias is the conv's bias repeated per phase: bias'[co*U + s] = bias[co].

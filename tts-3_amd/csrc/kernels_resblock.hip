@@ -20,12 +20,6 @@
 
 namespace tts {
 
-#ifndef XT_ABLATE
-#define XT_ABLATE 0  // timing-only builds (wrong results): 1 = conflict-free (misplaced) xt stores
-#endif
-// the 32 lanes of a half write rows l32 at one column position: dword 20 row + c, 8 banks (4-way);
-// the ablation adds (l32 >> 3) dwords so they cover 32 banks, to price the conflict
-#define XT_ABLATE_OFF (XT_ABLATE ? 4 * ((threadIdx.x & 31) >> 3) : 0)
 
 
 // Workgroup geometry (GEO): 4 waves as WM (row blocks) x WN (column groups), each wave TM x TN
@@ -105,7 +99,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
     const int ts = tx0 - a1.pad + r;
     const bool ok = r < XW && ts >= 0 && ts < T;
     uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
-    ulds[i] = r < XW ? r * S::ROWB + 8 * q : -1;
+    ulds[i] = r < XW ? r * S::ROWB + 8 * quad_pos(q) : -1;
   }
   f32x4 xall[ALLX ? NC : 1][P::UPT];
   auto load_x = [&](int c) {
@@ -253,24 +247,16 @@ void resblock_pair_kernel(ResPairArgs pa) {
       }
       tscale = ldexpf(1.f, -et);
     }
-    // xt pieces: row = convs1 column, group = co / 16; registers r, r+1 (r even) are channels
-    // co, co+1 -> one 32-bit store per piece
+    // xt pieces: row = convs1 column; registers 8 gl .. 8 gl + 7 are positions 8 half .. + 7 of
+    // group (m row block, gl) (quad_pos order): one 16-byte store per piece
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int row = xrow0 + n * 32;
+      for (int n = 0; n < TN; ++n)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          unsigned w[NP];
-          S::split2(acc[m][n][r] * tscale, acc[m][n][r + 1] * tscale, w);
-          unsigned char* dst = smem + ((co >> 4) * P::TROWS + row) * S::ROWB + 2 * (co & 15) + XT_ABLATE_OFF;
-#pragma unroll
-          for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];
-        }
-      }
+        for (int gl = 0; gl < 2; ++gl)
+          store_xt8<S>(smem + (((mrow0 + m * 32) / 16 + gl) * P::TROWS + xrow0 + n * 32) * S::ROWB + 16 * half,
+                       acc[m][n], 8 * gl, tscale);
     // zero rows RP_W .. TROWS-1 of every group (read only by the discarded columns)
     constexpr int ZB = (P::TROWS - RP_W) * S::ROWB;  // bytes per group
     for (int e = tid * 16; e < NC * ZB; e += 256 * 16) {
@@ -522,7 +508,7 @@ void resblock3_kernel(ResBlock3Args a) {
             v[j] = lrelu2(xv[g][i][j], 0.1f);
             if (H3) v[j] *= xs;
           }
-          split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * q, v[0], v[1], v[2], v[3]);
+          split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * quad_pos(q), v[0], v[1], v[2], v[3]);
         }
       }
     __builtin_amdgcn_sched_barrier(0);  // keep the loads below the window's use
@@ -625,19 +611,11 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int row = xcol0 + n * 32 + roff;
+      for (int n = 0; n < TN; ++n)
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          unsigned w[NP];
-          S::split2(acc[m][n][r] * scale, acc[m][n][r + 1] * scale, w);
-          unsigned char* dst = smem + ((co >> 4) * PR + row) * S::ROWB + 2 * (co & 15) + XT_ABLATE_OFF;
-#pragma unroll
-          for (int p = 0; p < NP; ++p)
-            *reinterpret_cast<unsigned*>(dst + 32 * p) = w[p];
-        }
-      }
+        for (int gl = 0; gl < 2; ++gl)
+          store_xt8<S>(smem + (((mrow0 + m * 32) / 16 + gl) * PR + xcol0 + n * 32 + roff) * S::ROWB + 16 * half,
+                       acc[m][n], 8 * gl, scale);
     // edge rows: [0, roff) and [roff + RP_W, PR) of every group
     constexpr int EB = 2 * R3_XOFF * S::ROWB;  // upper bound of edge bytes per group
     for (int e = tid * 16; e < NC * EB; e += NT * 16) {

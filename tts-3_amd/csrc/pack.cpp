@@ -78,7 +78,8 @@ int64_t packed_conv1d_split_numel(int mode, int Cout, int Cin, int K, const Conv
   return (mblocks * groups * K + 4) * split_pieces(mode) * 64 * 4;
 }
 
-int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f) {
+int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const ConvTile& t, float* out_f,
+                      bool quad_perm) {
   const int NP = split_pieces(mode);
   int e = 0;
   if (mode == MATH_FP32_F16X3) {
@@ -106,7 +107,8 @@ int pack_conv1d_split(int mode, const float* w, int Cout, int Cin, int K, const 
         for (int lane = 0; lane < 64; ++lane)
           for (int j = 0; j < 8; ++j) {
             const int co = mb * 32 + (lane & 31);
-            const int ci = c16 * 16 + 8 * (lane >> 5) + j;
+            const int pos = 8 * (lane >> 5) + j;  // MFMA k index = 16-bit position in the LDS row
+            const int ci = c16 * 16 + (quad_perm ? 4 * quad_pos(pos >> 2) + (pos & 3) : pos);
             const float v = (co < Cout && ci < Cin) ? w[((int64_t)co * Cin + ci) * K + k] : 0.f;
             if (NP == 3) split3_host(v, pc[0][lane][j], pc[1][lane][j], pc[2][lane][j]);
             else if (NP == 2) split_h3_host(std::ldexp(v, -e), pc[0][lane][j], pc[1][lane][j]);
@@ -193,7 +195,7 @@ int pack_conv1d_wino(int mode, const float* w, int Cout, int Cin, int K, const C
         const int ch = 4 * q + 2 * jp + e;
         std::copy_n(wt.data() + ((size_t)o * Cin + g * 16 + ch) * KS, KS, wp.data() + ((size_t)o * Cin + g * 16 + kk) * KS);
       }
-  return pack_conv1d_split(mode, wp.data(), Cout, Cin, KS, t, out);
+  return pack_conv1d_split(mode, wp.data(), Cout, Cin, KS, t, out, /*quad_perm=*/false);
 }
 
 }  // namespace tts

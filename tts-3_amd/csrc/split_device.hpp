@@ -110,6 +110,20 @@ __device__ __forceinline__ void split_store4(unsigned char* dst, float v0, float
   for (int p = 0; p < S::NP; ++p) *reinterpret_cast<u32x2*>(dst + 32 * p) = u32x2{w0[p], w1[p]};
 }
 
+// Accumulator registers r0 .. r0 + 7 of one lane (8 channels of one 16-channel group, positions
+// 8 half .. + 7 in quad_pos order) -> split pieces, one 16-byte store per piece at dst + 32 p
+// (dst: the lane's row, + 16 half).  8 consecutive lanes' rows cover the 32 banks (row pitch
+// ROWB / 4 = 4 x odd dwords): conflict-free.
+template <class S, class V>
+__device__ __forceinline__ void store_xt8(unsigned char* dst, const V& acc, int r0, float scale) {
+  unsigned w[4][S::NP];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) S::split2(acc[r0 + 2 * k] * scale, acc[r0 + 2 * k + 1] * scale, w[k]);
+#pragma unroll
+  for (int p = 0; p < S::NP; ++p)
+    *reinterpret_cast<u32x4_t*>(dst + 32 * p) = u32x4_t{w[0][p], w[1][p], w[2][p], w[3][p]};
+}
+
 // Exponent e such that max|x| * 2^-e lies in [2^13, 2^14): read the 64 max-abs slots the
 // producer published (one per lane), wave max, frexp.  No statistics, zero or non-finite max:
 // e = 0 (an overflowing input then yields inf, as fp16 would; NaN propagates).

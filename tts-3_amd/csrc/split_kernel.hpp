@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
     uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
-    ulds[i] = (g < G) ? (g * C::XROWS + r) * S::ROWB + 8 * q : -1;
+    ulds[i] = (g < G) ? (g * C::XROWS + r) * S::ROWB + 8 * quad_pos(q) : -1;
   }
 
   f32x4 xreg[C::UPT];

@@ -74,8 +74,10 @@ static void check_conv1d(int Cout, int Cin, int K, const ConvTile& t) {
 }
 
 // decode pack_conv1d_split's element (co, ci, k) back to fp32 (w' = w * 2^-e for f16x3)
+// quad_perm: position pos of a 16-channel group holds channel 4 quad_pos(pos / 4) + pos % 4 (the
+// split kernels' order, common.hpp); false for the Winograd packer (its own order, decoded by caller)
 static void check_split(int mode, const std::vector<float>& w, int Cout, int Cin, int K, const ConvTile& t,
-                        const std::vector<float>& packed, int e, const char* what) {
+                        const std::vector<float>& packed, int e, const char* what, bool quad_perm = true) {
   const int NP = mode == MATH_FP32_F16X3 ? 2 : (mode == MATH_BF16 ? 1 : 3);
   const uint16_t* p = reinterpret_cast<const uint16_t*>(packed.data());
   const int mblocks = ceil_div(Cout, t.BM) * (t.BM / 32), groups = ceil_div(Cin, t.CK) * (t.CK / 16);
@@ -85,7 +87,8 @@ static void check_split(int mode, const std::vector<float>& w, int Cout, int Cin
       for (int k = 0; k < K; ++k, ++step)
         for (int lane = 0; lane < 64; ++lane)
           for (int j = 0; j < 8; ++j) {
-            const int co = mb * 32 + (lane & 31), ci = c16 * 16 + 8 * (lane >> 5) + j;
+            const int pos = 8 * (lane >> 5) + j;
+            const int co = mb * 32 + (lane & 31), ci = c16 * 16 + (quad_perm ? 4 * quad_pos(pos >> 2) + (pos & 3) : pos);
             const float want = (co < Cout && ci < Cin) ? w[((size_t)co * Cin + ci) * K + k] : 0.f;
             auto piece = [&](int q) { return p[((step * NP + q) * 64 + lane) * 8 + j]; };
             double got;
@@ -170,7 +173,7 @@ static void check_wino(int Cout, int Cin, int K, const ConvTile& t) {
       const int kk = ci & 15, ch = (ci & ~15) + 4 * ((kk >> 1) & 3) + 2 * (kk >> 3) + (kk & 1);
       std::copy_n(u.data() + ((size_t)o * Cin + ch) * KS, KS, up.data() + ((size_t)o * Cin + ci) * KS);
     }
-  check_split(MATH_FP32_F16X3, up, Cout, Cin, KS, t, out, e, "pack_conv1d_wino");
+  check_split(MATH_FP32_F16X3, up, Cout, Cin, KS, t, out, e, "pack_conv1d_wino", /*quad_perm=*/false);
 }
 
 int main() {
