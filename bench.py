@@ -635,6 +635,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     faulthandler.dump_traceback_later(a.rank_timeout, exit=True)  # a hung peer ends this rank
+    # stdout carries exactly the one JSON line: whatever native libraries print there (RCCL's
+    # version banner at communicator setup) goes to stderr instead
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
+    def emit(rec):
+        os.write(json_fd, (json.dumps(rec) + "\n").encode())
+
     rehearse = a.rehearse_sharded and world == 1
     dist_on = world > 1 or rehearse
     if rehearse:  # a one-rank process group (no torchrun needed)
@@ -720,7 +729,7 @@ def main():
         rec["data"] = "STUB (test only): CPU stand-in vocoder, not a measurement"
         rec["dtype"] = "fp32"
         if rank == 0:
-            print(json.dumps(rec), flush=True)
+            emit(rec)
         if dist_on:
             dist.barrier()
             dist.destroy_process_group()
@@ -841,8 +850,8 @@ def main():
             "vits_waveform": vits,
             "accuracy_vs_fp64_oracle": acc,
         })
-        print(json.dumps(rec), flush=True)
-    if world > 1:
+        emit(rec)
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     faulthandler.cancel_dump_traceback_later()
