@@ -233,14 +233,34 @@ typedef struct TtsGlowEncoderCfg {
   int c_in_channels;        /* 0 = unconditioned; > 0: speaker vector size, the duration predictor reads
                                cat(x, g.expand(T)) (encoder.py:166-168; GlowTTS c_in_channels) */
   int math_mode;            /* TTS_MATH_FP32 (default), TTS_MATH_FP32_X6 or TTS_MATH_BF16 */
+  /* since ABI 113: the other encoder types of encoder.py:97-123 (0 = rel_pos_transformer) */
+  int encoder_type;         /* TTS_ENC_REL_POS_TRANSFORMER / _GATED_CONV / _RESIDUAL_CONV_BN / _TIME_DEPTH_SEPARABLE */
+  int num_conv_blocks;      /* residual_conv_bn: convs per residual block (2) */
+  int num_res_blocks;       /* residual_conv_bn: residual blocks (13) = entries of dilations */
+  int dilations[32];        /* residual_conv_bn: dilation of each residual block */
 } TtsGlowEncoderCfg;
 
-/* Host weight order (R = 2*rel_attn_window_size + 1, dk = hidden/num_heads, H = hidden):
+#define TTS_ENC_REL_POS_TRANSFORMER 0
+#define TTS_ENC_GATED_CONV 1          /* GatedConvBlock(H, kernel_size, dropout, num_layers), no prenet */
+#define TTS_ENC_RESIDUAL_CONV_BN 2    /* ResidualConv1dBNBlock + postnet conv1x1 -> BatchNorm */
+#define TTS_ENC_TIME_DEPTH_SEPARABLE 3 /* TimeDepthSeparableConvBlock (prenet as rel_pos) */
+
+/* Host weight order (R = 2*rel_attn_window_size + 1, dk = hidden/num_heads, H = hidden, k =
+ * kernel_size; a BatchNorm "BN(C)" is weight [C], bias [C], running_mean [C], running_var [C]):
  *   emb.weight [num_chars][H]
- *   if use_prenet: for l < 3: prenet.conv_layers.l.weight [H][H][5], bias [H],
+ *   if use_prenet (rel_pos_transformer, time_depth_separable):
+ *                  for l < 3: prenet.conv_layers.l.weight [H][H][5], bias [H],
  *                             prenet.norm_layers.l.gamma [H], beta [H]
  *                  prenet.proj.weight [H][H][1], bias [H]
- *   for l < num_layers (encoder.*):
+ *   gated_conv, for l < num_layers: encoder.conv_layers.l.weight [2H][H][k], bias [2H],
+ *                                   encoder.norm_layers.l.gamma [2H], beta [2H]
+ *   residual_conv_bn, for i < num_res_blocks, j < num_conv_blocks:
+ *       encoder.res_blocks.i.conv_bn_blocks.j.conv1d.weight [H][H][k], bias [H], .norm BN(H)
+ *     then postnet.0.weight [H][H][1], bias [H], postnet.1 BN(H)
+ *   time_depth_separable, for l < num_layers: encoder.layers.l.time_conv.weight [2H][H][1], bias [2H],
+ *       norm1 BN(2H), depth_conv.weight [H][1][k], bias [H], norm2 BN(H),
+ *       time_conv2.weight [H][H][1], bias [H], norm3 BN(H)
+ *   rel_pos_transformer, for l < num_layers (encoder.*):
  *       attn_layers.l.conv_q.weight [H][H][1], bias, conv_k.*, conv_v.*, conv_o.*
  *       if rel_attn_window_size: attn_layers.l.emb_rel_k [1][R][dk], emb_rel_v [1][R][dk]
  *       norm_layers_1.l.gamma [H], beta [H]

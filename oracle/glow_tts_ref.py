@@ -16,6 +16,11 @@ fp64): the rel_pos_transformer ``Encoder`` and the duration / alignment glue of
 * ``TTS/tts/layers/generic/normalization.py:23-28``  LayerNorm (channel axis, eps 1e-4)
 * ``TTS/tts/models/glow_tts.py:349-361``  durations, y_mask, generate_path, compute_outputs
   (:138-148), z; ``TTS/tts/utils/helpers.py:43-57`` sequence_mask, ``:154-169`` generate_path
+* the other encoder types (encoder.py:112-127): ``generic/gated_conv.py:27-36`` (conv on o * mask,
+  LayerNorm, GLU, residual), ``generic/res_conv_bn.py:39-44, :80-83, :119-127`` (unpadded conv,
+  zero pad (d(k-1)//2, rest), relu, BatchNorm; residual + mask per block; postnet conv1x1 ->
+  BatchNorm, * mask), ``generic/time_depth_sep_conv.py:44-56, :82-84`` (x * mask, conv1x1, BN,
+  GLU, depthwise conv, BN, swish, conv1x1, BN, residual)
 
 The relative-position terms are computed here directly from their definition (key j of query i
 uses embedding j - i + W when |j - i| <= W) instead of the reference's pad/reshape skew; the
@@ -77,18 +82,28 @@ def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None):
     return out.transpose(2, 3).contiguous().view(b, c, t)
 
 
+def _bn(x, w, pre, eps=1e-5):
+    """nn.BatchNorm1d in eval mode (running statistics)."""
+    return F.batch_norm(x, w[f"{pre}.running_mean"], w[f"{pre}.running_var"], w[f"{pre}.weight"], w[f"{pre}.bias"],
+                        False, 0.0, eps)
+
+
 def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: torch.Tensor,
                     hidden_channels: int = 192, encoder_params: Optional[dict] = None, mean_only: bool = True,
-                    use_prenet: bool = True, dtype=torch.float64, g: Optional[torch.Tensor] = None, **_unused):
+                    use_prenet: bool = True, dtype=torch.float64, g: Optional[torch.Tensor] = None,
+                    encoder_type: str = "rel_pos_transformer", **_unused):
     """Encoder.forward(x, x_lengths, g) -> (x_m, x_logs, logw, x_mask) (encoder.py:143-179); g [B, c_in, 1]
     is expanded over time and concatenated to the duration predictor's input (:166-168)."""
+    et = encoder_type.lower()
     ep = encoder_params or {"kernel_size": 3, "num_layers": 6, "num_heads": 2, "hidden_channels_ffn": 768}
-    w = {k: v.to(dtype) for k, v in sd.items()}
+    w = {k: v.to(dtype) if v.is_floating_point() else v for k, v in sd.items()}
     H = hidden_channels
     x = F.embedding(tokens, w["emb.weight"]) * math.sqrt(H)
     x = x.transpose(1, -1)
     x_mask = sequence_mask(lengths, x.size(2)).unsqueeze(1).to(dtype)
-    if use_prenet:  # glow.py:61-67
+    if et == "residual_conv_bn" and use_prenet:
+        raise TypeError("Sequential.forward() takes 2 positional arguments but 3 were given")  # encoder.py:158
+    if use_prenet and et in ("rel_pos_transformer", "time_depth_separable"):  # glow.py:61-67
         x_res = x
         for i in range(3):
             x = F.conv1d(x * x_mask, w[f"prenet.conv_layers.{i}.weight"], w[f"prenet.conv_layers.{i}.bias"], padding=2)
@@ -98,7 +113,40 @@ def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: 
         x = x * x_mask
     K = ep.get("kernel_size", 1)
     pl, pr = (K - 1) // 2, K // 2
-    for i in range(ep["num_layers"]):  # transformer.py:420-431
+    if et == "gated_conv":  # gated_conv.py:27-36 (dropout: identity at inference)
+        o = res = x
+        for i in range(ep["num_layers"]):
+            o = F.conv1d(o * x_mask, w[f"encoder.conv_layers.{i}.weight"], w[f"encoder.conv_layers.{i}.bias"],
+                         padding=K // 2)
+            o = layer_norm(o, w[f"encoder.norm_layers.{i}.gamma"], w[f"encoder.norm_layers.{i}.beta"])
+            o = res + F.glu(o, dim=1)
+            res = o
+        x = o
+    elif et == "residual_conv_bn":  # res_conv_bn.py:119-127, :80-83, :39-44; postnet encoder.py:161-162
+        o = x * x_mask
+        for i, d in enumerate(ep["dilations"]):
+            res = o
+            for j in range(ep.get("num_conv_blocks", 2)):
+                pre = f"encoder.res_blocks.{i}.conv_bn_blocks.{j}"
+                o = F.conv1d(o, w[f"{pre}.conv1d.weight"], w[f"{pre}.conv1d.bias"], dilation=d)
+                ptot = d * (K - 1)
+                o = F.pad(o, [ptot // 2, ptot - ptot // 2])
+                o = _bn(F.relu(o), w, f"{pre}.norm")
+            o = (o + res) * x_mask
+        x = _bn(F.conv1d(o, w["postnet.0.weight"], w["postnet.0.bias"]), w, "postnet.1") * x_mask
+    elif et == "time_depth_separable":  # time_depth_sep_conv.py:44-56, :82-84
+        for i in range(ep["num_layers"]):
+            pre = f"encoder.layers.{i}"
+            x = x * x_mask
+            h = _bn(F.conv1d(x, w[f"{pre}.time_conv.weight"], w[f"{pre}.time_conv.bias"]), w, f"{pre}.norm1")
+            h = F.glu(h, dim=1)
+            h = F.conv1d(h, w[f"{pre}.depth_conv.weight"], w[f"{pre}.depth_conv.bias"], padding=(K - 1) // 2,
+                         groups=H)
+            h = _bn(h, w, f"{pre}.norm2")
+            h = h * torch.sigmoid(h)
+            h = _bn(F.conv1d(h, w[f"{pre}.time_conv2.weight"], w[f"{pre}.time_conv2.bias"]), w, f"{pre}.norm3")
+            x = x + h
+    for i in range(ep["num_layers"] if et == "rel_pos_transformer" else 0):  # transformer.py:420-431
         pre = f"encoder.attn_layers.{i}"
         x = x * x_mask
         q = F.conv1d(x, w[f"{pre}.conv_q.weight"], w[f"{pre}.conv_q.bias"])

@@ -5,6 +5,7 @@ the GPU box):   python tests/golden/make_goldens.py        (HiFiGAN + Glow fixtu
                 python tests/golden/make_goldens.py vits   (VITS flow fixtures)
                 python tests/golden/make_goldens.py glow_tts (Glow-TTS encoder + inference glue)
                 python tests/golden/make_goldens.py glow_cond (speaker-conditioned Glow decoder)
+                python tests/golden/make_goldens.py glow_enc_types (gated / residual-BN / TDS encoders)
 
 Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
 but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
@@ -79,7 +80,7 @@ def import_reference_glow_tts():
 def _ref_encoder(Encoder, cfg, seed):
     torch.manual_seed(0)
     ref = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
-                  "rel_pos_transformer", dict(cfg["encoder_params"]), dropout_p_dp=0.1,
+                  cfg.get("encoder_type", "rel_pos_transformer"), dict(cfg["encoder_params"]), dropout_p_dp=0.1,
                   mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"],
                   c_in_channels=cfg.get("c_in_channels", 0))
     sd = synthetic.glow_encoder_state_dict(**cfg, seed=seed)
@@ -351,6 +352,8 @@ def main():
         return main_handoff()
     if len(sys.argv) > 1 and sys.argv[1] == "xtts":
         return main_xtts()
+    if len(sys.argv) > 1 and sys.argv[1] == "glow_enc_types":
+        return main_glow_enc_types()
     if len(sys.argv) > 1 and sys.argv[1] == "glow_tts_spk":
         return main_glow_tts_spk()
     if len(sys.argv) > 1 and sys.argv[1] == "glow_cond":
@@ -421,6 +424,25 @@ def main_glow_tts():
                                 "hidden_channels_ffn": 192, "rel_attn_window_size": 4},
                 mean_only=False, use_prenet=False)
     glow_encoder_case(Encoder, "glow_encoder_rel_b2_t19", rcfg, seed=97, B=2, T=19, lengths=[19, 11], tok_seed=43)
+
+
+def main_glow_enc_types():
+    """G13: the other Glow-TTS encoder types (encoder.py:112-127) with random BatchNorm statistics:
+    gated_conv (3 layers, k5), residual_conv_bn (k4 -- an even kernel -- dilations 1,2,4,1,2, no
+    prenet: the reference's prenet call raises), time_depth_separable (3 layers, k5, prenet)."""
+    Encoder, _, _, _ = import_reference_glow_tts()
+    base = dict(num_chars=30, out_channels=16, hidden_channels=64, hidden_channels_dp=48)
+    cases = [
+        ("glow_encoder_gated_b3_t37", dict(base, encoder_type="gated_conv", mean_only=False, use_prenet=True,
+                                           encoder_params={"kernel_size": 5, "dropout_p": 0.1, "num_layers": 3})),
+        ("glow_encoder_rescbn_b3_t37", dict(base, encoder_type="residual_conv_bn", mean_only=False, use_prenet=False,
+                                            encoder_params={"kernel_size": 4, "dilations": [1, 2, 4, 1, 2],
+                                                            "num_conv_blocks": 2, "num_res_blocks": 5})),
+        ("glow_encoder_tds_b3_t37", dict(base, encoder_type="time_depth_separable", mean_only=True, use_prenet=True,
+                                         encoder_params={"kernel_size": 5, "num_layers": 3})),
+    ]
+    for i, (name, cfg) in enumerate(cases):
+        glow_encoder_case(Encoder, name, cfg, seed=301 + i, B=3, T=37, lengths=[37, 29, 13], tok_seed=51 + i)
 
 
 def main_glow_tts_spk():

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == N.ABI_VERSION == 112
+    assert N.lib().tts_abi_version() == N.ABI_VERSION == 113
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -361,11 +361,50 @@ def test_glow_encoder_config_validation(over, code):
     assert e.value.code == code
 
 
-def test_glow_encoder_other_types_and_cpu_raise():
+ENC_TYPES = [
+    ("gated_conv", {"kernel_size": 5, "dropout_p": 0.1, "num_layers": 9}, True, 1 + 9 * 4 + 4 + 10),
+    ("residual_conv_bn", {"kernel_size": 4, "dilations": [1, 2, 4] * 4 + [1], "num_conv_blocks": 2,
+                          "num_res_blocks": 13}, False, 1 + 13 * 2 * 6 + 6 + 4 + 10),
+    ("time_depth_separable", {"kernel_size": 5, "num_layers": 9}, True, 1 + 14 + 9 * 18 + 4 + 10),
+]
+
+
+@pytest.mark.parametrize("et,ep,pre,nw", ENC_TYPES, ids=[t[0] for t in ENC_TYPES])
+def test_glow_encoder_other_types_inventory(et, ep, pre, nw):
+    """gated_conv / residual_conv_bn / time_depth_separable (encoder.py:112-127, the reference's
+    suggested encoder_params :59-75): the reference's key set (BatchNorm buffers included) loads
+    strictly, and every tensor handed to the C-ABI has the size it expects."""
+    from tts_amd.tts import Encoder
+
+    sd = synthetic.glow_encoder_state_dict(num_chars=40, out_channels=80, hidden_channels=192, hidden_channels_dp=256,
+                                           encoder_type=et, encoder_params=ep, mean_only=False, use_prenet=pre, seed=5)
+    e = Encoder(40, 80, 192, 256, et, ep, mean_only=False, use_prenet=pre)
+    e.load_state_dict(sd)
+    ws = e._weight_list()
+    assert len(ws) == N.lib().tts_glow_encoder_num_weights(ctypes.byref(e._cfg)) == nw
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_encoder_weight_numel(ctypes.byref(e._cfg), i) == w.size
+    tracked = sum(v.numel() for k, v in sd.items() if k.endswith("num_batches_tracked"))
+    assert sum(w.size for w in ws) == sum(v.numel() for v in sd.values()) - tracked
+
+
+def test_glow_encoder_types_and_cpu_raise():
     from tts_amd.tts import Encoder, GlowTTS
 
-    with pytest.raises(NotImplementedError):
-        Encoder(10, 80, 192, 256, "gated_conv", {"kernel_size": 5, "num_layers": 9})
+    with pytest.raises(ValueError, match="Unkown encoder type"):  # encoder.py:123, sic
+        Encoder(10, 80, 192, 256, "conformer", {})
+    # the reference calls residual_conv_bn's nn.Sequential prenet with (x, x_mask): TypeError in forward
+    e = Encoder(10, 80, 64, 48, "residual_conv_bn", {"kernel_size": 4, "dilations": [1], "num_conv_blocks": 2,
+                                                     "num_res_blocks": 1}, use_prenet=True)
+    with pytest.raises(TypeError):
+        e(torch.zeros(1, 8, dtype=torch.long), torch.tensor([8]))
+    c = N.TtsGlowEncoderCfg(num_chars=10, out_channels=80, hidden_channels=64, hidden_channels_dp=48,
+                            encoder_type=N.ENCODER_TYPES["residual_conv_bn"], kernel_size=4, num_conv_blocks=2,
+                            num_res_blocks=1)
+    c.dilations[0] = 9  # beyond the conv kernels' halo
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c.dilations[0], c.encoder_type = 1, 7
+    assert N.lib().tts_glow_encoder_num_weights(ctypes.byref(c)) == -N.TTS_ERR_INVALID
     m = GlowTTS(dict(num_chars=32))
     with pytest.raises(RuntimeError, match="ROCm"):
         m.inference(torch.zeros(1, 4, dtype=torch.long), {"x_lengths": torch.tensor([4])})

@@ -1,5 +1,6 @@
-"""Glow-TTS text side on MI355X: the rel_pos_transformer Encoder, the duration / alignment glue and
-GlowTTS.inference end to end (tokens -> mel), against the reference goldens and the oracle."""
+"""Glow-TTS text side on MI355X: the Encoder (rel_pos_transformer and the gated_conv /
+residual_conv_bn / time_depth_separable types), the duration / alignment glue and GlowTTS.inference
+end to end (tokens -> mel), against the reference goldens and the oracle."""
 import numpy as np
 import pytest
 import torch
@@ -27,7 +28,7 @@ MEL_REL_RMS = 5e-6
 
 def build_encoder(cfg, seed, device, math_mode="fp32x6"):
     e = Encoder(cfg["num_chars"], cfg["out_channels"], cfg["hidden_channels"], cfg["hidden_channels_dp"],
-                "rel_pos_transformer", cfg["encoder_params"], mean_only=cfg["mean_only"],
+                cfg.get("encoder_type", "rel_pos_transformer"), cfg["encoder_params"], mean_only=cfg["mean_only"],
                 use_prenet=cfg["use_prenet"], c_in_channels=cfg.get("c_in_channels", 0), math_mode=math_mode)
     e.load_state_dict(synthetic.glow_encoder_state_dict(**cfg, seed=seed))
     e.eval()
@@ -93,6 +94,42 @@ def test_encoder_vs_oracle(cuda_device, B, T, lengths, window, mode):
                                        use_prenet=True)
     for n, o, r in zip(["x_m", "x_logs", "logw"], outs, ref):
         assert_close_fp32(o.cpu(), r, f"{n} B={B} T={T}", ENC_MAX_ABS, ENC_REL_RMS)
+
+
+ENC_TYPE_CFGS = {
+    "gated_conv": dict(encoder_params={"kernel_size": 5, "dropout_p": 0.1, "num_layers": 3}, use_prenet=True),
+    "residual_conv_bn": dict(encoder_params={"kernel_size": 4, "dilations": [1, 2, 4], "num_conv_blocks": 2,
+                                             "num_res_blocks": 3}, use_prenet=False),
+    "time_depth_separable": dict(encoder_params={"kernel_size": 5, "num_layers": 3}, use_prenet=True),
+}
+
+
+@pytest.mark.parametrize("et", list(ENC_TYPE_CFGS))
+@pytest.mark.parametrize("B,T,lengths", [(1, 13, [13]), (2, 70, [70, 33]), (3, 130, [130, 129, 16])])
+@pytest.mark.parametrize("mode", ["fp32", "fp32x6"])
+def test_encoder_types_vs_oracle(cuda_device, et, B, T, lengths, mode):
+    """The other encoder types at the default width (H = 192: 2H = 384-channel LayerNorm / GLU)
+    on ragged batches; the shortest span the residual_conv_bn kernels allow (3 * 4 + 1 tokens)."""
+    cfg = dict(GLOW_TTS_ENCODER, num_chars=50, encoder_type=et, mean_only=False, **ENC_TYPE_CFGS[et])
+    e = build_encoder(cfg, 11 + T, cuda_device, mode)
+    tok = synthetic.tokens(B, T, 50, seed=T + 1)
+    lens = torch.tensor(lengths)
+    outs = e(tok.to(cuda_device), lens.to(cuda_device))
+    sd = synthetic.glow_encoder_state_dict(**cfg, seed=11 + T)
+    ref = glow_tts_ref.encoder_forward(sd, tok, lens, hidden_channels=192, encoder_params=cfg["encoder_params"],
+                                       mean_only=False, use_prenet=cfg["use_prenet"], encoder_type=et)
+    for n, o, r in zip(["x_m", "x_logs", "logw"], outs, ref):
+        assert_close_fp32(o.cpu(), r, f"{et} {n} B={B} T={T}", ENC_MAX_ABS, ENC_REL_RMS)
+
+
+def test_encoder_residual_bn_too_short_raises(cuda_device):
+    """the reference's unpadded dilated conv raises on fewer tokens than its span (res_conv_bn.py:39)"""
+    cfg = dict(GLOW_TTS_ENCODER, num_chars=50, encoder_type="residual_conv_bn", mean_only=False,
+               **ENC_TYPE_CFGS["residual_conv_bn"])
+    e = build_encoder(cfg, 3, cuda_device, "fp32")
+    tok = synthetic.tokens(1, 12, 50, seed=1).to(cuda_device)
+    with pytest.raises(N.NativeError):
+        e(tok, torch.tensor([12], device=cuda_device))
 
 
 @pytest.mark.parametrize("name,meta,arr", GTTS, ids=[g[0] for g in GTTS])

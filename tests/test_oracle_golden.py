@@ -166,7 +166,8 @@ GTTS = goldens("glow_tts")
 
 def _enc_args(cfg):
     return dict(hidden_channels=cfg["hidden_channels"], encoder_params=cfg["encoder_params"],
-                mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"])
+                mean_only=cfg["mean_only"], use_prenet=cfg["use_prenet"],
+                encoder_type=cfg.get("encoder_type", "rel_pos_transformer"))
 
 
 @pytest.mark.parametrize("name,meta,arr", GENC + [(n, dict(m, config=m["encoder"], seed=m["eseed"]), a)

@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 112; }
+int tts_abi_version(void) { return 113; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN

@@ -1,9 +1,12 @@
-// Glow-TTS Encoder (rel_pos_transformer) executor: every matmul of the reference runs on the
-// conv kernels (1x1 q|k|v as one 3H-row conv, conv_o with the residual fused, FFN k3 with the
-// relu and the mask fused, prenet k5, duration predictor k3), the rest on kernels_text.hip.
-// Reference: TTS/tts/layers/glow_tts/encoder.py:143-179, glow.py:55-67 (prenet),
+// Glow-TTS Encoder executor: every matmul of the reference runs on the conv kernels (1x1 q|k|v
+// as one 3H-row conv, conv_o with the residual fused, FFN k3 with the relu and the mask fused,
+// prenet k5, duration predictor k3), the rest on kernels_text.hip.
+// Reference: TTS/tts/layers/glow_tts/encoder.py:97-179, glow.py:55-67 (prenet),
 // transformer.py:117-201 (attention), :319-341 (FFN), :415-432 (layer loop),
-// duration_predictor.py:47-73, normalization.py:23-28.
+// duration_predictor.py:47-73, normalization.py:23-28; the other encoder types:
+// generic/gated_conv.py:15-36, generic/res_conv_bn.py:19-127, generic/time_depth_sep_conv.py:5-84.
+// BatchNorms (eval) that directly follow a conv are folded into it on the host; the one after a
+// relu (Conv1dBN, res_conv_bn.py:43-44) runs as a per-channel affine.
 //
 // Masking: the reference masks conv INPUTS (x * x_mask); here every producer masks its output
 // instead (conv epilogue mask, LayerNorm * mask).  Padded positions never reach a valid one
@@ -18,20 +21,44 @@ namespace tts {
 
 namespace {
 int heads_dk(const TtsGlowEncoderCfg& c) { return c.hidden_channels / c.num_heads; }
+constexpr double kBnEps = 1e-5;  // nn.BatchNorm1d default
+// residual_conv_bn convs run with an odd kernel: an even reference kernel gets a zero tap appended
+int odd_k(int k) { return k % 2 ? k : k + 1; }
 }  // namespace
 
 std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
   std::vector<int64_t> n;
   const int64_t H = c.hidden_channels, F = c.hidden_channels_ffn, K = c.kernel_size, D = c.hidden_channels_dp;
+  const int et = c.encoder_type;
   n.push_back((int64_t)c.num_chars * H);  // emb.weight
-  if (c.use_prenet) {
+  auto bn = [&](int64_t C) { for (int i = 0; i < 4; ++i) n.push_back(C); };
+  if (c.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {
     for (int l = 0; l < 3; ++l) {
       n.push_back(H * H * 5); n.push_back(H);  // prenet.conv_layers.l
       n.push_back(H); n.push_back(H);          // prenet.norm_layers.l gamma, beta
     }
     n.push_back(H * H); n.push_back(H);        // prenet.proj
   }
-  for (int l = 0; l < c.num_layers; ++l) {
+  if (et == TTS_ENC_GATED_CONV) {
+    for (int l = 0; l < c.num_layers; ++l) {
+      n.push_back(2 * H * H * K); n.push_back(2 * H);  // encoder.conv_layers.l
+      n.push_back(2 * H); n.push_back(2 * H);          // encoder.norm_layers.l
+    }
+  } else if (et == TTS_ENC_RESIDUAL_CONV_BN) {
+    for (int i = 0; i < c.num_res_blocks; ++i)
+      for (int j = 0; j < c.num_conv_blocks; ++j) {
+        n.push_back(H * H * K); n.push_back(H);  // res_blocks.i.conv_bn_blocks.j.conv1d
+        bn(H);                                   // .norm
+      }
+    n.push_back(H * H); n.push_back(H); bn(H);   // postnet.0 (conv1x1), postnet.1 (BatchNorm)
+  } else if (et == TTS_ENC_TIME_DEPTH_SEPARABLE) {
+    for (int l = 0; l < c.num_layers; ++l) {
+      n.push_back(2 * H * H); n.push_back(2 * H); bn(2 * H);  // time_conv, norm1
+      n.push_back(H * K); n.push_back(H); bn(H);              // depth_conv, norm2
+      n.push_back(H * H); n.push_back(H); bn(H);              // time_conv2, norm3
+    }
+  }
+  for (int l = 0; et == TTS_ENC_REL_POS_TRANSFORMER && l < c.num_layers; ++l) {
     for (int j = 0; j < 4; ++j) { n.push_back(H * H); n.push_back(H); }  // conv_q, conv_k, conv_v, conv_o
     if (c.rel_attn_window_size > 0) {
       const int64_t R = 2 * c.rel_attn_window_size + 1;
@@ -52,15 +79,37 @@ std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
 }
 
 void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
-  TTS_REQUIRE(c.num_chars >= 1 && c.out_channels >= 1 && c.hidden_channels >= 1 && c.hidden_channels_dp >= 1 &&
-                  c.hidden_channels_ffn >= 1 && c.num_layers >= 1,
-              1, "bad Glow encoder configuration");
-  TTS_REQUIRE(c.num_heads >= 1 && c.hidden_channels % c.num_heads == 0, 1,
-              "channels should be divisible by num_heads (transformer.py:75)");
-  TTS_REQUIRE(heads_dk(c) <= 128, 3, "attention head size above 128 is not implemented");
-  TTS_REQUIRE(c.kernel_size == 1 || c.kernel_size == 3 || c.kernel_size == 5 || c.kernel_size == 7 ||
-                  c.kernel_size == 11,
-              3, "FFN kernel_size must be 1, 3, 5, 7 or 11");
+  const int et = c.encoder_type;
+  TTS_REQUIRE(et >= TTS_ENC_REL_POS_TRANSFORMER && et <= TTS_ENC_TIME_DEPTH_SEPARABLE, 1, "unknown encoder_type");
+  TTS_REQUIRE(c.num_chars >= 1 && c.out_channels >= 1 && c.hidden_channels >= 1 && c.hidden_channels_dp >= 1, 1,
+              "bad Glow encoder configuration");
+  const auto kset = [](int k) { return k == 1 || k == 3 || k == 5 || k == 7 || k == 11; };
+  if (et == TTS_ENC_GATED_CONV) {
+    TTS_REQUIRE(c.num_layers >= 1, 1, "gated_conv: num_layers must be >= 1");
+    TTS_REQUIRE(kset(c.kernel_size), 3, "gated_conv: kernel_size must be 1, 3, 5, 7 or 11");
+    TTS_REQUIRE(c.hidden_channels % 16 == 0 && 2 * c.hidden_channels <= 768, 3,
+                "gated_conv: hidden_channels must be a multiple of 16 and at most 384");
+  } else if (et == TTS_ENC_RESIDUAL_CONV_BN) {
+    TTS_REQUIRE(c.num_res_blocks >= 1 && c.num_res_blocks <= 32 && c.num_conv_blocks >= 1, 1,
+                "residual_conv_bn: 1..32 residual blocks (one dilation each) of >= 1 convs");
+    TTS_REQUIRE(kset(odd_k(c.kernel_size)), 3, "residual_conv_bn: kernel_size must be 1-7, 10 or 11");
+    for (int i = 0; i < c.num_res_blocks; ++i)
+      TTS_REQUIRE(c.dilations[i] >= 1 && (odd_k(c.kernel_size) - 1) * c.dilations[i] <= (odd_k(c.kernel_size) - 1) * 5, 3,
+                  "residual_conv_bn: dilations must be 1..5");
+    TTS_REQUIRE(!c.use_prenet, 1,
+                "residual_conv_bn with use_prenet: the reference calls its nn.Sequential prenet with (x, x_mask) "
+                "and raises TypeError (encoder.py:158)");
+  } else if (et == TTS_ENC_TIME_DEPTH_SEPARABLE) {
+    TTS_REQUIRE(c.num_layers >= 2, 1, "time_depth_separable: num_layers must be > 1 (time_depth_sep_conv.py:64)");
+    TTS_REQUIRE(c.kernel_size % 2 == 1 && c.kernel_size <= 31, 3,
+                "time_depth_separable: kernel_size must be odd (time_depth_sep_conv.py:63) and <= 31");
+  } else {
+    TTS_REQUIRE(c.hidden_channels_ffn >= 1 && c.num_layers >= 1, 1, "bad Glow encoder configuration");
+    TTS_REQUIRE(c.num_heads >= 1 && c.hidden_channels % c.num_heads == 0, 1,
+                "channels should be divisible by num_heads (transformer.py:75)");
+    TTS_REQUIRE(heads_dk(c) <= 128, 3, "attention head size above 128 is not implemented");
+    TTS_REQUIRE(kset(c.kernel_size), 3, "FFN kernel_size must be 1, 3, 5, 7 or 11");
+  }
   TTS_REQUIRE(c.rel_attn_window_size >= 0, 1, "rel_attn_window_size must be >= 0 (0 = None)");
   TTS_REQUIRE(c.c_in_channels >= 0, 1, "c_in_channels must be >= 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
@@ -89,24 +138,39 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
     fix.push_back({off, dst});
   };
   // conv from one or more row blocks of torch weights [rows][Cin][K] stacked along Cout
+  // conv from one or more row blocks of torch weights [rows][Cin][k] stacked along Cout; kc > k
+  // appends zero taps (an even reference kernel on the odd-kernel conv); bn (weight, bias, mean,
+  // var) folds a following BatchNorm into the weights and bias
   auto put_conv = [&](Conv& cv, std::vector<std::pair<const float*, const float*>> parts, int rows_each, int Cin,
-                      int k) {
+                      int k, int dil = 1, int pad = -1, int kc = 0, const float* const* bn = nullptr) {
     const int Cout = rows_each * (int)parts.size();
-    cv.Cin = Cin; cv.Cout = Cout; cv.K = k;
+    kc = kc ? kc : k;
+    cv.Cin = Cin; cv.Cout = Cout; cv.K = kc; cv.dil = dil;
+    cv.pad = pad >= 0 ? pad : dil * (k - 1) / 2;
     // text batches are short (a 16 x 128-token batch is 2,048 columns): the split modes take the
     // 32x128 tile (4 waves side by side) so a conv launches Cout/32 x B workgroups, not Cout/128 x B
-    cv.tile = is_split_mode(mode) ? 16 : conv_tile_for(mode, Cout, k, Cin, 1, false);
+    cv.tile = is_split_mode(mode) ? 16 : conv_tile_for(mode, Cout, kc, Cin, dil, false);
     const ConvTile t = conv_tile(mode, cv.tile);
     cv.n_chunks = ceil_div(Cin, t.CK);
-    std::vector<float> w((size_t)Cout * Cin * k), b(Cout);
+    std::vector<float> w((size_t)Cout * Cin * kc, 0.f), b(Cout);
     for (size_t p = 0; p < parts.size(); ++p) {
-      std::memcpy(w.data() + p * (size_t)rows_each * Cin * k, parts[p].first, sizeof(float) * rows_each * Cin * k);
+      for (int r = 0; r < rows_each; ++r)
+        for (int ci = 0; ci < Cin; ++ci)
+          std::memcpy(w.data() + (((size_t)p * rows_each + r) * Cin + ci) * kc,
+                      parts[p].first + ((size_t)r * Cin + ci) * k, sizeof(float) * k);
       std::memcpy(b.data() + p * rows_each, parts[p].second, sizeof(float) * rows_each);
     }
-    const size_t n = packed_conv_numel(mode, Cout, Cin, k, t);
+    if (bn) {  // y = (conv - mean) / sqrt(var + eps) * gamma + beta, in double
+      for (int co = 0; co < Cout; ++co) {
+        const double sc = (double)bn[0][co] / std::sqrt((double)bn[3][co] + kBnEps);
+        for (size_t i = 0; i < (size_t)Cin * kc; ++i) w[(size_t)co * Cin * kc + i] = (float)(w[(size_t)co * Cin * kc + i] * sc);
+        b[co] = (float)(((double)b[co] - bn[2][co]) * sc + bn[1][co]);
+      }
+    }
+    const size_t n = packed_conv_numel(mode, Cout, Cin, kc, t);
     const size_t off = host.size();
     host.resize(off + align(n), 0.f);
-    const int w_exp = pack_conv(mode, w.data(), Cout, Cin, k, t, host.data() + off);
+    const int w_exp = pack_conv(mode, w.data(), Cout, Cin, kc, t, host.data() + off);
     TTS_REQUIRE(w_exp == 0, 3, "Glow encoder: scaled weight packing is not supported");
     fix.push_back({off, &cv.w});
     const size_t nb = (size_t)ceil_div(Cout, t.BM) * t.BM;
@@ -120,9 +184,22 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
     put(bt, C, &n.beta);
   };
 
+  // BatchNorm (weight, bias, running_mean, running_var) -> device scale / shift
+  auto put_affine = [&](Affine& af, const float* const* bn, int C) {
+    std::vector<float> sc(C), sh(C);
+    for (int c = 0; c < C; ++c) {
+      const double s = (double)bn[0][c] / std::sqrt((double)bn[3][c] + kBnEps);
+      sc[c] = (float)s;
+      sh[c] = (float)((double)bn[1][c] - (double)bn[2][c] * s);
+    }
+    put(sc.data(), C, &af.scale);
+    put(sh.data(), C, &af.shift);
+  };
+  const int et = cfg_.encoder_type;
+
   size_t wi = 0;
   put(hw[wi++], (size_t)cfg_.num_chars * H, &emb_);
-  if (cfg_.use_prenet) {
+  if (cfg_.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {
     for (int l = 0; l < 3; ++l) {
       put_conv(pre_conv_[l], {{hw[wi], hw[wi + 1]}}, H, H, 5);
       put_norm(pre_norm_[l], hw[wi + 2], hw[wi + 3], H);
@@ -131,8 +208,53 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
     put_conv(pre_proj_, {{hw[wi], hw[wi + 1]}}, H, H, 1);
     wi += 2;
   }
-  layers_.resize(cfg_.num_layers);
-  for (int l = 0; l < cfg_.num_layers; ++l) {
+  if (et == TTS_ENC_GATED_CONV) {
+    gconv_.resize(cfg_.num_layers);
+    gnorm_.resize(cfg_.num_layers);
+    for (int l = 0; l < cfg_.num_layers; ++l) {
+      put_conv(gconv_[l], {{hw[wi], hw[wi + 1]}}, 2 * H, H, K);
+      put_norm(gnorm_[l], hw[wi + 2], hw[wi + 3], 2 * H);
+      wi += 4;
+    }
+  } else if (et == TTS_ENC_RESIDUAL_CONV_BN) {
+    const int k = cfg_.kernel_size;
+    rcbn_.resize((size_t)cfg_.num_res_blocks * cfg_.num_conv_blocks);
+    for (int i = 0; i < cfg_.num_res_blocks; ++i) {
+      const int d = cfg_.dilations[i];
+      const int ptot = d * (k - 1), ps = ptot / 2;  // ZeroPad (pad_s, pad_e) of the conv's output
+      for (int j = 0; j < cfg_.num_conv_blocks; ++j) {
+        ConvBN& cb = rcbn_[(size_t)i * cfg_.num_conv_blocks + j];
+        put_conv(cb.conv, {{hw[wi], hw[wi + 1]}}, H, H, k, d, ps, odd_k(k));
+        put_affine(cb.bn, hw + wi + 2, H);
+        cb.lo = ps;
+        cb.hi = ptot - ps;
+        wi += 6;
+      }
+    }
+    put_conv(post_, {{hw[wi], hw[wi + 1]}}, H, H, 1, 1, 0, 0, hw + wi + 2);
+    wi += 6;
+  } else if (et == TTS_ENC_TIME_DEPTH_SEPARABLE) {
+    const int k = cfg_.kernel_size;
+    tds_.resize(cfg_.num_layers);
+    for (int l = 0; l < cfg_.num_layers; ++l) {
+      TdsLayer& L = tds_[l];
+      put_conv(L.time_conv, {{hw[wi], hw[wi + 1]}}, 2 * H, H, 1, 1, 0, 0, hw + wi + 2);
+      wi += 6;
+      std::vector<float> dw((size_t)H * k), db(H);  // depth_conv with norm2 folded
+      for (int c = 0; c < H; ++c) {
+        const double sc = (double)hw[wi + 2][c] / std::sqrt((double)hw[wi + 5][c] + kBnEps);
+        for (int j = 0; j < k; ++j) dw[(size_t)c * k + j] = (float)(hw[wi][(size_t)c * k + j] * sc);
+        db[c] = (float)(((double)hw[wi + 1][c] - hw[wi + 4][c]) * sc + hw[wi + 3][c]);
+      }
+      put(dw.data(), dw.size(), &L.dw_w);
+      put(db.data(), db.size(), &L.dw_b);
+      wi += 6;
+      put_conv(L.time_conv2, {{hw[wi], hw[wi + 1]}}, H, H, 1, 1, 0, 0, hw + wi + 2);
+      wi += 6;
+    }
+  }
+  layers_.resize(et == TTS_ENC_REL_POS_TRANSFORMER ? cfg_.num_layers : 0);
+  for (int l = 0; l < (int)layers_.size(); ++l) {
     Layer& L = layers_[l];
     put_conv(L.qkv, {{hw[wi], hw[wi + 1]}, {hw[wi + 2], hw[wi + 3]}, {hw[wi + 4], hw[wi + 5]}}, H, H, 1);
     put_conv(L.o, {{hw[wi + 6], hw[wi + 7]}}, H, H, 1);
@@ -215,7 +337,7 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
     Conv1dArgs a{};
     a.x = in; a.w = cv.w; a.bias = cv.b; a.y = out; a.res = res; a.mask = m;
     a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = T; a.Tout = T;
-    a.dil = 1; a.pad = (cv.K - 1) / 2; a.rep_pad = 0; a.n_chunks = cv.n_chunks;  // same padding (transformer.py:335)
+    a.dil = cv.dil; a.pad = cv.pad; a.rep_pad = 0; a.n_chunks = cv.n_chunks;  // same padding (transformer.py:335)
     a.in_slope = 1.f; a.out_slope = out_slope; a.zmode = 0; a.zdiv = 1.f;
     a.mask_res = mask_res ? 1 : 0;
     run(prof, s, name, 2.0 * P * cv.Cout * cv.Cin * cv.K, 4.0 * P * (cv.Cin + cv.Cout + (res ? cv.Cout : 0)),
@@ -231,7 +353,8 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
   run(prof, s, "enc_embed", 0.0, 4.0 * P * H + 16.0 * P,
       [&] { launch_embed(tok, len, emb_, X0, x_mask, B, H, T, cfg_.num_chars, scale, s); });
   float* x = X0;
-  if (cfg_.use_prenet) {  // glow.py:61-67
+  const int et = cfg_.encoder_type;
+  if (cfg_.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {  // glow.py:61-67
     const float* in = X0;
     for (int l = 0; l < 3; ++l) {
       conv("enc_prenet_conv", pre_conv_[l], in, Wd, nullptr, mask, 1.f, false);
@@ -241,8 +364,59 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
     conv("enc_prenet_proj", pre_proj_, Nb, X1, X0, mask, 1.f, true);  // (x_res + proj(x)) * mask
     x = X1;
   }
+  if (et == TTS_ENC_GATED_CONV) {
+    // gated_conv.py:30-36: o = o + glu(LN(conv(o * mask))); x is masked on entry and every layer
+    // output is masked (the reference's o differs only at padded positions, which the next conv
+    // and every returned tensor multiply by x_mask)
+    for (int l = 0; l < cfg_.num_layers; ++l) {
+      conv("enc_gated_conv", gconv_[l], x, Wd, nullptr, nullptr, 1.f, false);
+      run(prof, s, "enc_layernorm_glu", 0.0, 4.0 * P * 3 * H,
+          [&] { launch_layernorm_glu(Wd, x, gnorm_[l].gamma, gnorm_[l].beta, mask, x, B, 2 * H, T, kEps, s); });
+    }
+  } else if (et == TTS_ENC_RESIDUAL_CONV_BN) {
+    // res_conv_bn.py:119-127: o = x * mask; per block: o = (convbn^n(o) + o) * mask.  Inside a
+    // block nothing is masked (the reference's second conv reads the first one's BatchNorm output
+    // at padded positions too)
+    float* o = x;
+    float* t1 = (x == X0) ? X1 : X0;
+    const int nb = cfg_.num_conv_blocks;
+    for (int i = 0; i < cfg_.num_res_blocks; ++i) {
+      const float* in = o;
+      for (int j = 0; j < nb; ++j) {
+        const ConvBN& cb = rcbn_[(size_t)i * nb + j];
+        const bool last = j + 1 == nb;
+        float* dst = last ? t1 : (j % 2 ? A : Wd);
+        TTS_REQUIRE(T > cb.lo + cb.hi, 3,
+                    "residual_conv_bn: fewer tokens than the dilated kernel spans (the reference's conv raises)");
+        conv("enc_res_conv", cb.conv, in, dst, nullptr, nullptr, 1.f, false);
+        run(prof, s, "enc_bn_act", 0.0, 4.0 * P * H * (last ? 4 : 2), [&] {
+          launch_bn_act(dst, cb.bn.scale, cb.bn.shift, last ? o : nullptr, last ? mask : nullptr, dst, B, H, T, cb.lo,
+                        T - cb.hi, s);
+        });
+        in = dst;
+      }
+      std::swap(o, t1);
+    }
+    // postnet: conv1x1 -> BatchNorm (folded), * x_mask (encoder.py:161-162)
+    float* px = (o == X0) ? X1 : X0;
+    conv("enc_postnet", post_, o, px, nullptr, mask, 1.f, false);
+    x = px;
+  } else if (et == TTS_ENC_TIME_DEPTH_SEPARABLE) {
+    // time_depth_sep_conv.py:44-56, :82-84: x = layer(x * mask) = x*mask + tc2(swish(dw(glu(tc(x*mask)))));
+    // inputs are masked by their producer; the glu / depthwise stage is not masked (the
+    // reference's depthwise conv reads it at padded positions)
+    for (int l = 0; l < cfg_.num_layers; ++l) {
+      const TdsLayer& L = tds_[l];
+      float* other = (x == X0) ? X1 : X0;
+      conv("enc_tds_time_conv", L.time_conv, x, Wd, nullptr, nullptr, 1.f, false);
+      run(prof, s, "enc_tds_glu_dw_swish", 2.0 * P * H * cfg_.kernel_size, 4.0 * P * 3 * H,
+          [&] { launch_glu_dw_swish(Wd, L.dw_w, L.dw_b, A, B, H, T, cfg_.kernel_size, s); });
+      conv("enc_tds_time_conv2", L.time_conv2, A, other, x, mask, 1.f, true);  // (x + tc2(.)) * mask
+      x = other;
+    }
+  }
   // transformer layers (transformer.py:420-431); x is masked on entry
-  for (int l = 0; l < cfg_.num_layers; ++l) {
+  for (int l = 0; l < (int)layers_.size(); ++l) {
     const Layer& L = layers_[l];
     float* other = (x == X0) ? X1 : X0;
     conv("enc_qkv", L.qkv, x, Wd, nullptr, nullptr, 1.f, false);

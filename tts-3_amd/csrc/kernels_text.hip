@@ -124,6 +124,140 @@ void launch_layernorm(const float* a, const float* r, const float* gamma, const 
 }
 
 // ---------------------------------------------------------------------------------------
+// gated_conv layer tail (gated_conv.py:30-36): LayerNorm over the conv's 2H channels, GLU over
+// the channel halves, residual add; the layer's next conv reads o * x_mask, so the output is
+// masked here.  Same slicing as layernorm_kernel: channels c and c + C/2 sit in one thread when
+// C/2 is a multiple of LN_S.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) layernorm_glu_kernel(const float* a, const float* res,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ mask, float* y, int C, int T,
+                                                            float eps) {
+  __shared__ float part[LN_S][LN_T];
+  const int b = blockIdx.y;
+  const int col = threadIdx.x & (LN_T - 1);
+  const int sl = threadIdx.x / LN_T;
+  const int t = blockIdx.x * LN_T + col;
+  const bool ok = t < T;
+  const int Ch = C / 2;
+  const size_t base = (size_t)b * C * T + (ok ? t : 0);
+  const size_t hbase = (size_t)b * Ch * T + (ok ? t : 0);
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    v[i] = 0.f;
+    if (c < C) {
+      v[i] = a[base + (size_t)c * T];
+      s += v[i];
+    }
+  }
+  part[sl][col] = s;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_S; ++i) tot += part[i][col];
+  const float mean = tot / (float)C;
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    if (c < C) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+  }
+  part[sl][col] = q;
+  __syncthreads();
+  float qt = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_S; ++i) qt += part[i][col];
+  const float var = qt / (float)C;
+  const float rs = 1.f / sqrtf(var + eps);
+  const float m = mask ? mask[(size_t)b * T + (ok ? t : 0)] : 1.f;
+  if (!ok) return;
+  const int ih = Ch / LN_S;  // slice offset of channel c + C/2
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = sl + i * LN_S;
+    if (c < Ch && i + ih < LN_MAXV) {
+      const int c2 = c + Ch;
+      const float o1 = (v[i] - mean) * rs * gamma[c] + beta[c];
+      const float o2 = (v[i + ih] - mean) * rs * gamma[c2] + beta[c2];
+      const float g = o1 * (1.f / (1.f + expf(-o2)));
+      y[hbase + (size_t)c * T] = (res[hbase + (size_t)c * T] + g) * m;
+    }
+  }
+}
+
+void launch_layernorm_glu(const float* a, const float* res, const float* gamma, const float* beta, const float* mask,
+                          float* y, int B, int C, int T, float eps, hipStream_t s) {
+  TTS_REQUIRE(C <= LN_S * LN_MAXV && C % (2 * LN_S) == 0, 3,
+              "gated_conv LayerNorm: 2 x hidden channels must be a multiple of 32 and at most 768");
+  dim3 grid(ceil_div(T, LN_T), B);
+  hipLaunchKernelGGL(layernorm_glu_kernel, grid, dim3(256), 0, s, a, res, gamma, beta, mask, y, C, T, eps);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------
+// Conv1dBN tail (res_conv_bn.py:39-44) and the residual block's add + mask (:124-127)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bn_act_kernel(const float* a, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, const float* res,
+                                                     const float* __restrict__ mask, float* y, int C, int T, int lo,
+                                                     int hi) {
+  const int b = blockIdx.z, c = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  const size_t i = ((size_t)b * C + c) * T + t;
+  const float v = (t >= lo && t < hi) ? fmaxf(a[i], 0.f) : 0.f;
+  float o = v * scale[c] + shift[c];
+  if (res) o = (o + res[i]) * mask[(size_t)b * T + t];
+  y[i] = o;
+}
+
+void launch_bn_act(const float* a, const float* scale, const float* shift, const float* res, const float* mask,
+                   float* y, int B, int C, int T, int lo, int hi, hipStream_t s) {
+  TTS_REQUIRE(!res || mask, 1, "bn_act: the residual form needs the mask");
+  dim3 grid(ceil_div(T, 256), C, B);
+  hipLaunchKernelGGL(bn_act_kernel, grid, dim3(256), 0, s, a, scale, shift, res, mask, y, C, T, lo, hi);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------
+// TimeDepthSeparableConv middle (time_depth_sep_conv.py:50-54): GLU, depthwise conv (norm2
+// folded), swish.  One thread per output; the GLU of each tap's input is recomputed (k <= 11).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) glu_dw_swish_kernel(const float* __restrict__ a, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, float* __restrict__ y,
+                                                           int C, int T, int k) {
+  const int b = blockIdx.z, c = blockIdx.y;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  const float* a1 = a + ((size_t)b * 2 * C + c) * T;
+  const float* a2 = a1 + (size_t)C * T;
+  const int p = (k - 1) / 2;
+  float v = 0.f;
+  for (int j = 0; j < k; ++j) {
+    const int ts = t - p + j;
+    if (ts >= 0 && ts < T) v = fmaf(w[c * k + j], a1[ts] * (1.f / (1.f + expf(-a2[ts]))), v);
+  }
+  v += bias[c];
+  y[((size_t)b * C + c) * T + t] = v * (1.f / (1.f + expf(-v)));
+}
+
+void launch_glu_dw_swish(const float* a, const float* w, const float* bias, float* y, int B, int C, int T, int k,
+                         hipStream_t s) {
+  TTS_REQUIRE(k >= 1 && k <= 31 && k % 2 == 1, 3, "time_depth_separable: kernel_size must be odd and <= 31");
+  dim3 grid(ceil_div(T, 256), C, B);
+  hipLaunchKernelGGL(glu_dw_swish_kernel, grid, dim3(256), 0, s, a, w, bias, y, C, T, k);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------
 // Relative-position multi-head self-attention (transformer.py:142-180), one workgroup per
 // (8 queries, head, utterance):
 //   s[i][j] = (q_i . k_j) / sqrt(dk) + [|j-i| <= W] (q_i . ek[j-i+W]) / sqrt(dk)

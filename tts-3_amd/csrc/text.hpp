@@ -20,6 +20,20 @@ void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, floa
 // y = LN_C(a [+ r]) * gamma + beta [relu] * mask (mask may be NULL); y may alias a or r
 void launch_layernorm(const float* a, const float* r, const float* gamma, const float* beta, const float* mask,
                       float* y, int B, int C, int T, float eps, bool relu, hipStream_t s);
+// gated_conv layer tail: y[c] = (res[c] + LN(a)[c] * sigmoid(LN(a)[c + C/2])) * mask for c < C/2,
+// LN over the C channels of a (gamma, beta [C]); y may alias res
+void launch_layernorm_glu(const float* a, const float* res, const float* gamma, const float* beta, const float* mask,
+                          float* y, int B, int C, int T, float eps, hipStream_t s);
+// Conv1dBN tail (res_conv_bn.py:39-44): v = t in [lo, hi) ? relu(a) : 0 (the zero-padded border of
+// the unpadded conv); y = v * scale[c] + shift[c] (BatchNorm, eval); then, with res: y = (y + res)
+// * mask (the residual block's add and mask, :124-127).  y may alias a.
+void launch_bn_act(const float* a, const float* scale, const float* shift, const float* res, const float* mask,
+                   float* y, int B, int C, int T, int lo, int hi, hipStream_t s);
+// TimeDepthSeparableConv middle (time_depth_sep_conv.py:50-54): u = glu(a) over a's 2C channels,
+// v = depthwise conv k (weights [C][k] and bias with norm2 folded in, zero padding (k-1)/2),
+// y = v * sigmoid(v)
+void launch_glu_dw_swish(const float* a, const float* w, const float* bias, float* y, int B, int C, int T, int k,
+                         hipStream_t s);
 // out[B][H][T] = multi-head attention of qkv [B][3H][T] (W = 0: no relative embeddings)
 void launch_attention(const float* qkv, const float* mask, const float* ek, const float* ev, float* out, int B,
                       int H, int heads, int T, int W, hipStream_t s);
@@ -63,9 +77,23 @@ class GlowEncoder {
 
  private:
   struct Conv {
-    int Cin = 0, Cout = 0, K = 1, tile = 0, n_chunks = 0;
+    int Cin = 0, Cout = 0, K = 1, tile = 0, n_chunks = 0, dil = 1, pad = 0;
     float* w = nullptr;
     float* b = nullptr;
+  };
+  struct Affine {  // BatchNorm (eval) as y = x * scale + shift
+    float* scale = nullptr;
+    float* shift = nullptr;
+  };
+  struct ConvBN {  // residual_conv_bn: conv (k padded to an odd size) -> border zero -> relu -> BN
+    Conv conv;
+    Affine bn;
+    int lo = 0, hi = 0;  // valid output window offsets: [lo, T - hi)
+  };
+  struct TdsLayer {  // time_depth_separable (BatchNorms folded into the convs)
+    Conv time_conv, time_conv2;
+    float* dw_w = nullptr;
+    float* dw_b = nullptr;
   };
   struct Norm {
     float* gamma = nullptr;
@@ -85,6 +113,11 @@ class GlowEncoder {
   Conv pre_conv_[3], pre_proj_;
   Norm pre_norm_[3];
   std::vector<Layer> layers_;
+  std::vector<Conv> gconv_;        // gated_conv layers
+  std::vector<Norm> gnorm_;
+  std::vector<ConvBN> rcbn_;       // residual_conv_bn: num_res_blocks x num_conv_blocks
+  Conv post_;                      // residual_conv_bn postnet (BatchNorm folded)
+  std::vector<TdsLayer> tds_;
   Conv proj_m_, proj_s_, dp1_, dp2_, dp_proj_;
   Norm dpn1_, dpn2_;
   float* arena_ = nullptr;

@@ -29,7 +29,7 @@ TTS_ERR_OOM = 4
 MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
 # the C-ABI revision these bindings were written for (tts_abi_version() in csrc/abi.cpp)
-ABI_VERSION = 112
+ABI_VERSION = 113
 
 
 def default_math_mode(fp32_faithful_only: bool = True) -> str:
@@ -101,7 +101,15 @@ class TtsGlowEncoderCfg(Structure):
         ("use_prenet", c_int),
         ("c_in_channels", c_int),
         ("math_mode", c_int),
+        ("encoder_type", c_int),
+        ("num_conv_blocks", c_int),
+        ("num_res_blocks", c_int),
+        ("dilations", c_int * 32),
     ]
+
+
+# TtsGlowEncoderCfg.encoder_type (include/tts_mi355x.h TTS_ENC_*)
+ENCODER_TYPES = {"rel_pos_transformer": 0, "gated_conv": 1, "residual_conv_bn": 2, "time_depth_separable": 3}
 
 
 class TtsAudioNormCfg(Structure):

@@ -278,10 +278,11 @@ def glow_encoder_state_dict(
     c_in_channels: int = 0,
     seed: int = 8642,
     log_duration: float = 1.6,
+    encoder_type: str = "rel_pos_transformer",
     **_unused,
 ) -> "OrderedDict[str, torch.Tensor]":
-    """State dict of a Glow-TTS ``Encoder`` (TTS/tts/layers/glow_tts/encoder.py:83-152,
-    rel_pos_transformer) with synthetic weights, in the reference's key order.
+    """State dict of a Glow-TTS ``Encoder`` (TTS/tts/layers/glow_tts/encoder.py:83-152, any
+    ``encoder_type``) with synthetic weights, in the reference's key order.
 
     * embedding ~ N(0, H^-0.5) as the reference (:102), so emb * sqrt(H) has unit variance
     * convs variance-preserving (1x1 q/k/v/o, FFN k3, duration predictor k3); the prenet's
@@ -289,21 +290,25 @@ def glow_encoder_state_dict(
     * LayerNorm gamma ~ 1 + 0.1 N, beta ~ 0.1 N (reference init 0.1 / 0: a weak test)
     * duration ``proj`` bias = ``log_duration`` with small weights, so exp(logw) - 1 is a few
       frames per token (a random-init predictor clamps every duration to 1)
+    * BatchNorms (gated / residual / time-depth-separable encoders): weight ~ 1 + 0.1 N, bias and
+      running mean ~ 0.1 N, running var ~ exp(0.2 N) (the reference's init, 1 / 0 / 0 / 1, is the
+      identity)
     """
-    ep = dict(GLOW_TTS_ENCODER["encoder_params"]) if encoder_params is None else dict(encoder_params)
+    et = encoder_type.lower()
+    if encoder_params is None:
+        ep = dict(GLOW_TTS_ENCODER["encoder_params"]) if et == "rel_pos_transformer" else {}
+    else:
+        ep = dict(encoder_params)
     rng = np.random.default_rng(seed)
     sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
     H = hidden_channels
-    F_ = ep["hidden_channels_ffn"]
     K = ep.get("kernel_size", 1)
-    nh = ep["num_heads"]
-    W = ep.get("rel_attn_window_size")
 
     def t(a):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
 
-    def conv(name: str, cout: int, cin: int, k: int, scale: float = 1.0, bias_std: float = 0.02):
-        w = rng.standard_normal((cout, cin, k)) * (scale / np.sqrt(cin * k))
+    def conv(name: str, cout: int, cin: int, k: int, scale: float = 1.0, bias_std: float = 0.02, groups: int = 1):
+        w = rng.standard_normal((cout, cin // groups, k)) * (scale / np.sqrt(cin // groups * k))
         sd[f"{name}.weight"] = t(w)
         sd[f"{name}.bias"] = t(rng.standard_normal((cout,)) * bias_std)
 
@@ -311,13 +316,58 @@ def glow_encoder_state_dict(
         sd[f"{name}.gamma"] = t(1.0 + 0.1 * rng.standard_normal((1, c, 1)))
         sd[f"{name}.beta"] = t(0.1 * rng.standard_normal((1, c, 1)))
 
-    sd["emb.weight"] = t(rng.standard_normal((num_chars, H)) * H**-0.5)
-    if use_prenet:
+    def bnorm(name: str, c: int):  # BatchNorm1d (eval): random affine and running statistics
+        sd[f"{name}.weight"] = t(1.0 + 0.1 * rng.standard_normal((c,)))
+        sd[f"{name}.bias"] = t(0.1 * rng.standard_normal((c,)))
+        sd[f"{name}.running_mean"] = t(0.1 * rng.standard_normal((c,)))
+        sd[f"{name}.running_var"] = t(np.exp(0.2 * rng.standard_normal((c,))))
+        sd[f"{name}.num_batches_tracked"] = torch.tensor(0)
+
+    def prenet_rcln():
         for l in range(3):
             conv(f"prenet.conv_layers.{l}", H, H, 5)
         for l in range(3):
             norm(f"prenet.norm_layers.{l}", H)
         conv("prenet.proj", H, H, 1, 0.5)
+
+    sd["emb.weight"] = t(rng.standard_normal((num_chars, H)) * H**-0.5)
+    if et != "rel_pos_transformer":
+        if et == "gated_conv":  # generic/gated_conv.py:21-24 (no prenet, encoder.py:112-113)
+            for l in range(ep["num_layers"]):
+                conv(f"encoder.conv_layers.{l}", 2 * H, H, K, 0.7)
+            for l in range(ep["num_layers"]):
+                norm(f"encoder.norm_layers.{l}", 2 * H)
+        elif et == "residual_conv_bn":  # generic/res_conv_bn.py; encoder.py:114-120
+            if use_prenet:
+                conv("prenet.0", H, H, 1)
+            for i in range(len(ep["dilations"])):
+                for j in range(ep.get("num_conv_blocks", 2)):
+                    pre = f"encoder.res_blocks.{i}.conv_bn_blocks.{j}"
+                    conv(f"{pre}.conv1d", H, H, K, 0.6)
+                    bnorm(f"{pre}.norm", H)
+            conv("postnet.0", H, H, 1)
+            bnorm("postnet.1", H)
+        elif et == "time_depth_separable":  # generic/time_depth_sep_conv.py; encoder.py:121-127
+            if use_prenet:
+                prenet_rcln()
+            for l in range(ep["num_layers"]):
+                pre = f"encoder.layers.{l}"
+                conv(f"{pre}.time_conv", 2 * H, H, 1)
+                bnorm(f"{pre}.norm1", 2 * H)
+                conv(f"{pre}.depth_conv", H, H, K, 1.0, groups=H)
+                bnorm(f"{pre}.norm2", H)
+                conv(f"{pre}.time_conv2", H, H, 1, 0.5)
+                bnorm(f"{pre}.norm3", H)
+        else:
+            raise ValueError(f"unknown encoder_type {encoder_type}")
+        _glow_encoder_heads(sd, conv, norm, t, H, out_channels, hidden_channels_dp, mean_only, c_in_channels,
+                            log_duration)
+        return sd
+    F_ = ep["hidden_channels_ffn"]
+    nh = ep["num_heads"]
+    W = ep.get("rel_attn_window_size")
+    if use_prenet:
+        prenet_rcln()
     for l in range(ep["num_layers"]):
         pre = f"encoder.attn_layers.{l}"
         for n in ("q", "k", "v", "o"):
@@ -333,6 +383,14 @@ def glow_encoder_state_dict(
         conv(f"encoder.ffn_layers.{l}.conv_2", H, F_, K)
     for l in range(ep["num_layers"]):
         norm(f"encoder.norm_layers_2.{l}", H)
+    _glow_encoder_heads(sd, conv, norm, t, H, out_channels, hidden_channels_dp, mean_only, c_in_channels,
+                        log_duration)
+    return sd
+
+
+def _glow_encoder_heads(sd, conv, norm, t, H, out_channels, hidden_channels_dp, mean_only, c_in_channels,
+                        log_duration):
+    """proj_m / proj_s and the duration predictor (encoder.py:128-141), shared by every encoder type."""
     conv("proj_m", out_channels, H, 1)
     if not mean_only:
         conv("proj_s", out_channels, H, 1, 0.3)
@@ -342,7 +400,6 @@ def glow_encoder_state_dict(
     norm("duration_predictor.norm_2", hidden_channels_dp)
     conv("duration_predictor.proj", 1, hidden_channels_dp, 1, 0.3)
     sd["duration_predictor.proj.bias"] = t(np.full((1,), log_duration))
-    return sd
 
 
 def tokens(batch: int, length: int, num_chars: int, seed: int = 0) -> torch.Tensor:

@@ -1,11 +1,11 @@
 """Drop-in Glow-TTS text side whose inference runs in ``libtts_mi355x.so``.
 
-* ``Encoder`` mirrors ``TTS/tts/layers/glow_tts/encoder.py`` (Coqui TTS 0.22.0) for
-  ``encoder_type="rel_pos_transformer"``: same constructor (:83-95), same parameter tree
-  (``emb``, ``prenet.{conv_layers,norm_layers,proj}``, ``encoder.{attn_layers,norm_layers_1,
-  ffn_layers,norm_layers_2}``, ``proj_m``, ``proj_s``, ``duration_predictor.*``) so reference
-  checkpoints load unchanged; ``forward(x, x_lengths, g=None)`` returns
-  ``(x_m, x_logs, logw, x_mask)`` like :143-179.
+* ``Encoder`` mirrors ``TTS/tts/layers/glow_tts/encoder.py`` (Coqui TTS 0.22.0) for every
+  ``encoder_type`` (:97-123): ``rel_pos_transformer`` (the Glow-TTS default), ``gated_conv``,
+  ``residual_conv_bn`` and ``time_depth_separable``; same constructor (:83-95), same parameter
+  tree (``emb``, ``prenet.*``, ``encoder.*``, ``postnet.*``, ``proj_m``, ``proj_s``,
+  ``duration_predictor.*``) so reference checkpoints load unchanged; ``forward(x, x_lengths,
+  g=None)`` returns ``(x_m, x_logs, logw, x_mask)`` like :143-179.
 * ``GlowTTS`` is the inference surface of ``TTS/tts/models/glow_tts.py``: ``inference(x,
   aux_input)`` (:342-374) runs encoder -> durations -> alignment expansion -> decoder reverse
   on the device and returns the reference's output dict.  ``load_checkpoint`` (:522-530) reads
@@ -13,9 +13,8 @@
 
 The nn modules below only hold parameters; the handle is rebuilt when any parameter changes.
 Multi-speaker models (``use_speaker_embedding`` / ``use_d_vector_file``, glow_tts.py:107-191)
-condition the duration predictor and the decoder flows on ``g``.  The other encoder types
-(gated_conv, residual_conv_bn, time_depth_separable) and training (``forward``, MAS) are
-outside the MI355X path and raise.
+condition the duration predictor and the decoder flows on ``g``.  Training (``forward``, MAS)
+is outside the MI355X path.
 """
 from __future__ import annotations
 
@@ -116,6 +115,92 @@ class RelativePositionTransformer(nn.Module):
             self.norm_layers_2.append(LayerNorm(out_channels if last else hidden_channels))
 
 
+class GatedConvBlock(nn.Module):
+    """generic/gated_conv.py:6-25 (parameters only)."""
+
+    def __init__(self, in_out_channels, kernel_size, dropout_p, num_layers):
+        super().__init__()
+        self.dropout_p = dropout_p
+        self.num_layers = num_layers
+        self.kernel_size = kernel_size
+        self.conv_layers = nn.ModuleList()
+        self.norm_layers = nn.ModuleList()
+        self.layers = nn.ModuleList()
+        for _ in range(num_layers):
+            self.conv_layers += [nn.Conv1d(in_out_channels, 2 * in_out_channels, kernel_size,
+                                           padding=kernel_size // 2)]
+            self.norm_layers += [LayerNorm(2 * in_out_channels)]
+
+
+class Conv1dBN(nn.Module):
+    """generic/res_conv_bn.py:19-44 (parameters only): conv (no padding) -> zero pad -> relu -> BN."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, dilation):
+        super().__init__()
+        self.conv1d = nn.Conv1d(in_channels, out_channels, kernel_size, dilation=dilation)
+        self.norm = nn.BatchNorm1d(out_channels)
+
+
+class Conv1dBNBlock(nn.Module):
+    """generic/res_conv_bn.py:47-83 (parameters only)."""
+
+    def __init__(self, in_channels, out_channels, hidden_channels, kernel_size, dilation, num_conv_blocks=2):
+        super().__init__()
+        self.conv_bn_blocks = nn.Sequential(*[
+            Conv1dBN(in_channels if idx == 0 else hidden_channels,
+                     out_channels if idx == (num_conv_blocks - 1) else hidden_channels, kernel_size, dilation)
+            for idx in range(num_conv_blocks)])
+
+
+class ResidualConv1dBNBlock(nn.Module):
+    """generic/res_conv_bn.py:86-127 (parameters only)."""
+
+    def __init__(self, in_channels, out_channels, hidden_channels, kernel_size, dilations, num_res_blocks=13,
+                 num_conv_blocks=2):
+        super().__init__()
+        assert len(dilations) == num_res_blocks
+        self.kernel_size = kernel_size
+        self.dilations = list(dilations)
+        self.num_conv_blocks = num_conv_blocks
+        self.res_blocks = nn.ModuleList([
+            Conv1dBNBlock(in_channels if idx == 0 else hidden_channels,
+                          out_channels if (idx + 1) == len(dilations) else hidden_channels, hidden_channels,
+                          kernel_size, dilation, num_conv_blocks)
+            for idx, dilation in enumerate(dilations)])
+
+
+class TimeDepthSeparableConv(nn.Module):
+    """generic/time_depth_sep_conv.py:5-56 (parameters only)."""
+
+    def __init__(self, in_channels, hid_channels, out_channels, kernel_size, bias=True):
+        super().__init__()
+        self.time_conv = nn.Conv1d(in_channels, 2 * hid_channels, kernel_size=1, stride=1, padding=0, bias=bias)
+        self.norm1 = nn.BatchNorm1d(2 * hid_channels)
+        self.depth_conv = nn.Conv1d(hid_channels, hid_channels, kernel_size, stride=1,
+                                    padding=(kernel_size - 1) // 2, groups=hid_channels, bias=bias)
+        self.norm2 = nn.BatchNorm1d(hid_channels)
+        self.time_conv2 = nn.Conv1d(hid_channels, out_channels, kernel_size=1, stride=1, padding=0, bias=bias)
+        self.norm3 = nn.BatchNorm1d(out_channels)
+
+
+class TimeDepthSeparableConvBlock(nn.Module):
+    """generic/time_depth_sep_conv.py:59-84 (parameters only)."""
+
+    def __init__(self, in_channels, hid_channels, out_channels, num_layers, kernel_size, bias=True):
+        super().__init__()
+        assert (kernel_size - 1) % 2 == 0
+        assert num_layers > 1
+        self.kernel_size = kernel_size
+        self.layers = nn.ModuleList()
+        self.layers.append(TimeDepthSeparableConv(in_channels, hid_channels,
+                                                  out_channels if num_layers == 1 else hid_channels, kernel_size,
+                                                  bias))
+        for idx in range(num_layers - 1):
+            self.layers.append(TimeDepthSeparableConv(
+                hid_channels, hid_channels, out_channels if (idx + 1) == (num_layers - 1) else hid_channels,
+                kernel_size, bias))
+
+
 class DurationPredictor(nn.Module):
     """duration_predictor.py:7-73 (parameters only)."""
 
@@ -136,9 +221,9 @@ class Encoder(nn.Module):
     def __init__(self, num_chars, out_channels, hidden_channels, hidden_channels_dp, encoder_type, encoder_params,
                  dropout_p_dp=0.1, mean_only=False, use_prenet=True, c_in_channels=0, math_mode: str = "fp32x6"):
         super().__init__()
-        if encoder_type.lower() != "rel_pos_transformer":
-            raise NotImplementedError(f"encoder_type '{encoder_type}' is not implemented on the MI355X path "
-                                      "(only rel_pos_transformer, the Glow-TTS default)")
+        et = encoder_type.lower()
+        if et not in N.ENCODER_TYPES:
+            raise ValueError(" [!] Unkown encoder type.")  # encoder.py:123
         if math_mode not in N.MATH_MODES:
             raise ValueError(f"math_mode must be one of {sorted(N.MATH_MODES)}")
         self.num_chars = num_chars
@@ -153,10 +238,22 @@ class Encoder(nn.Module):
         self.math_mode = math_mode
         self.emb = nn.Embedding(num_chars, hidden_channels)
         nn.init.normal_(self.emb.weight, 0.0, hidden_channels**-0.5)
-        if use_prenet:
-            self.prenet = ResidualConv1dLayerNormBlock(hidden_channels, hidden_channels, hidden_channels,
-                                                       kernel_size=5, num_layers=3, dropout_p=0.5)
-        self.encoder = RelativePositionTransformer(hidden_channels, hidden_channels, hidden_channels, **encoder_params)
+        H = hidden_channels
+        if et == "rel_pos_transformer":  # encoder.py:104-111
+            if use_prenet:
+                self.prenet = ResidualConv1dLayerNormBlock(H, H, H, kernel_size=5, num_layers=3, dropout_p=0.5)
+            self.encoder = RelativePositionTransformer(H, H, H, **encoder_params)
+        elif et == "gated_conv":  # :112-113
+            self.encoder = GatedConvBlock(H, **encoder_params)
+        elif et == "residual_conv_bn":  # :114-120
+            if use_prenet:
+                self.prenet = nn.Sequential(nn.Conv1d(H, H, 1), nn.ReLU())
+            self.encoder = ResidualConv1dBNBlock(H, H, H, **encoder_params)
+            self.postnet = nn.Sequential(nn.Conv1d(H, H, 1), nn.BatchNorm1d(H))
+        else:  # time_depth_separable, :121-127
+            if use_prenet:
+                self.prenet = ResidualConv1dLayerNormBlock(H, H, H, kernel_size=5, num_layers=3, dropout_p=0.5)
+            self.encoder = TimeDepthSeparableConvBlock(H, H, H, **encoder_params)
         self.proj_m = nn.Conv1d(hidden_channels, out_channels, 1)
         if not mean_only:
             self.proj_s = nn.Conv1d(hidden_channels, out_channels, 1)
@@ -168,13 +265,28 @@ class Encoder(nn.Module):
         c.out_channels = out_channels
         c.hidden_channels = hidden_channels
         c.hidden_channels_dp = hidden_channels_dp
-        c.hidden_channels_ffn = ep["hidden_channels_ffn"]
-        c.num_heads = ep["num_heads"]
-        c.num_layers = ep["num_layers"]
-        c.kernel_size = ep.get("kernel_size", 1)
-        c.rel_attn_window_size = ep.get("rel_attn_window_size") or 0
+        c.encoder_type = N.ENCODER_TYPES[et]
+        c.kernel_size = self.encoder.kernel_size if et != "rel_pos_transformer" else ep.get("kernel_size", 1)
+        if et == "rel_pos_transformer":
+            c.hidden_channels_ffn = ep["hidden_channels_ffn"]
+            c.num_heads = ep["num_heads"]
+            c.num_layers = ep["num_layers"]
+            c.rel_attn_window_size = ep.get("rel_attn_window_size") or 0
+        elif et == "residual_conv_bn":
+            d = self.encoder.dilations
+            if len(d) > 32:
+                raise NotImplementedError("residual_conv_bn: more than 32 residual blocks")
+            c.num_res_blocks = len(d)
+            c.num_conv_blocks = self.encoder.num_conv_blocks
+            for i, v in enumerate(d):
+                c.dilations[i] = int(v)
+        else:
+            c.num_layers = len(self.encoder.layers) if et == "time_depth_separable" else self.encoder.num_layers
         c.mean_only = 1 if mean_only else 0
-        c.use_prenet = 1 if use_prenet else 0
+        # residual_conv_bn: the reference calls its nn.Sequential prenet with (x, x_mask) and raises
+        # TypeError in forward (encoder.py:158); this module raises the same there
+        self._prenet_typeerror = et == "residual_conv_bn" and use_prenet
+        c.use_prenet = 1 if (use_prenet and not self._prenet_typeerror) else 0
         c.c_in_channels = c_in_channels
         c.math_mode = N.MATH_MODES[math_mode]
         self._cfg = c
@@ -194,13 +306,36 @@ class Encoder(nn.Module):
         def norm(m):
             ws.extend([_f32(m.gamma).reshape(-1), _f32(m.beta).reshape(-1)])
 
-        if self.use_prenet:
+        def bn(m):
+            ws.extend([_f32(m.weight), _f32(m.bias), _f32(m.running_mean), _f32(m.running_var)])
+
+        et = self.encoder_type.lower()
+        if self.use_prenet and et in ("rel_pos_transformer", "time_depth_separable"):
             for l in range(3):
                 conv(self.prenet.conv_layers[l])
                 norm(self.prenet.norm_layers[l])
             conv(self.prenet.proj)
         enc = self.encoder
-        for l in range(enc.num_layers):
+        if et == "gated_conv":
+            for l in range(enc.num_layers):
+                conv(enc.conv_layers[l])
+                norm(enc.norm_layers[l])
+        elif et == "residual_conv_bn":
+            for blk in enc.res_blocks:
+                for cb in blk.conv_bn_blocks:
+                    conv(cb.conv1d)
+                    bn(cb.norm)
+            conv(self.postnet[0])
+            bn(self.postnet[1])
+        elif et == "time_depth_separable":
+            for L in enc.layers:
+                conv(L.time_conv)
+                bn(L.norm1)
+                conv(L.depth_conv)
+                bn(L.norm2)
+                conv(L.time_conv2)
+                bn(L.norm3)
+        for l in range(enc.num_layers if et == "rel_pos_transformer" else 0):
             a = enc.attn_layers[l]
             for m in (a.conv_q, a.conv_k, a.conv_v, a.conv_o):
                 conv(m)
@@ -230,7 +365,8 @@ class Encoder(nn.Module):
         return dev
 
     def _native_handle(self):
-        key = tuple((p.data_ptr(), p._version, p.device) for p in self.parameters())
+        # BatchNorm running statistics are buffers: part of the key too
+        key = tuple((p.data_ptr(), p._version, p.device) for p in list(self.parameters()) + list(self.buffers()))
         if self._handle is not None and key == self._handle_key:
             return self._handle
         self._release()
@@ -296,6 +432,8 @@ class Encoder(nn.Module):
         """encoder.py:143-179: x [B, T] token ids, x_lengths [B], g [B, c_in, 1] (speaker vector of a
         c_in_channels > 0 encoder, concatenated to the duration predictor's input, :166-168)
         -> (x_m, x_logs, logw, x_mask)."""
+        if self._prenet_typeerror:
+            raise TypeError("Sequential.forward() takes 2 positional arguments but 3 were given")
         with torch.no_grad():
             h = self._native_handle()
             dev, tok, lens, gv, outs = self._io(x, x_lengths, g)
