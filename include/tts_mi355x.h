@@ -238,6 +238,9 @@ typedef struct TtsGlowEncoderCfg {
   int num_conv_blocks;      /* residual_conv_bn: convs per residual block (2) */
   int num_res_blocks;       /* residual_conv_bn: residual blocks (13) = entries of dilations */
   int dilations[32];        /* residual_conv_bn: dilation of each residual block */
+  int layer_norm_type;      /* rel_pos_transformer: 1 (LayerNorm, eps 1e-4; 0 = 1) or 2 (LayerNorm2, eps 1e-5) */
+  int has_input_length;     /* rel_pos_transformer: 1 when input_length is set (transformer.py:148-150): */
+  int input_length;         /*   scores with |i - j| > input_length are -1e4 (block-limited attention) */
 } TtsGlowEncoderCfg;
 
 #define TTS_ENC_REL_POS_TRANSFORMER 0

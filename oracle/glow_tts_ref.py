@@ -48,8 +48,9 @@ def layer_norm(x, gamma, beta, eps=1e-4):
     return (x - mean) * torch.rsqrt(var + eps) * gamma + beta
 
 
-def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None):
-    """q, k, v [B, C, T], mask [B, 1, T] -> [B, C, T] (transformer.py:142-180)."""
+def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None, input_length=None):
+    """q, k, v [B, C, T], mask [B, 1, T] -> [B, C, T] (transformer.py:142-180); input_length: the
+    block mask of :148-150 (scores outside |i - j| <= input_length are -1e4)."""
     b, c, t = q.shape
     dk = c // num_heads
     qh = q.view(b, num_heads, dk, t).transpose(2, 3)
@@ -67,6 +68,9 @@ def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None):
         scores = scores + loc / math.sqrt(dk)
     am = mask.unsqueeze(2) * mask.unsqueeze(-1)  # transformer.py:419
     scores = scores.masked_fill(am == 0, -1e4)
+    if input_length is not None:
+        band = (torch.arange(t)[None, :] - torch.arange(t)[:, None]).abs() <= input_length
+        scores = scores.masked_fill(~band, -1e4)
     p = F.softmax(scores, dim=-1)
     out = torch.matmul(p, vh)
     if emb_rel_v is not None:
@@ -146,20 +150,25 @@ def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: 
             h = h * torch.sigmoid(h)
             h = _bn(F.conv1d(h, w[f"{pre}.time_conv2.weight"], w[f"{pre}.time_conv2.bias"]), w, f"{pre}.norm3")
             x = x + h
+    # LayerNorm2 (layer_norm_type "2", normalization.py:42-53): F.layer_norm, eps 1e-5
+    eps_tf = 1e-5 if ep.get("layer_norm_type", "1") == "2" else 1e-4
     for i in range(ep["num_layers"] if et == "rel_pos_transformer" else 0):  # transformer.py:420-431
         pre = f"encoder.attn_layers.{i}"
         x = x * x_mask
         q = F.conv1d(x, w[f"{pre}.conv_q.weight"], w[f"{pre}.conv_q.bias"])
         k = F.conv1d(x, w[f"{pre}.conv_k.weight"], w[f"{pre}.conv_k.bias"])
         v = F.conv1d(x, w[f"{pre}.conv_v.weight"], w[f"{pre}.conv_v.bias"])
-        a = rel_attention(q, k, v, x_mask, ep["num_heads"], w.get(f"{pre}.emb_rel_k"), w.get(f"{pre}.emb_rel_v"))
+        a = rel_attention(q, k, v, x_mask, ep["num_heads"], w.get(f"{pre}.emb_rel_k"), w.get(f"{pre}.emb_rel_v"),
+                          ep.get("input_length"))
         y = F.conv1d(a, w[f"{pre}.conv_o.weight"], w[f"{pre}.conv_o.bias"])
-        x = layer_norm(x + y, w[f"encoder.norm_layers_1.{i}.gamma"], w[f"encoder.norm_layers_1.{i}.beta"])
+        x = layer_norm(x + y, w[f"encoder.norm_layers_1.{i}.gamma"].reshape(1, -1, 1),
+                       w[f"encoder.norm_layers_1.{i}.beta"].reshape(1, -1, 1), eps_tf)
         f = f"encoder.ffn_layers.{i}"
         y = F.conv1d(F.pad(x * x_mask, [pl, pr]), w[f"{f}.conv_1.weight"], w[f"{f}.conv_1.bias"])
         y = torch.relu(y)
         y = F.conv1d(F.pad(y * x_mask, [pl, pr]), w[f"{f}.conv_2.weight"], w[f"{f}.conv_2.bias"]) * x_mask
-        x = layer_norm(x + y, w[f"encoder.norm_layers_2.{i}.gamma"], w[f"encoder.norm_layers_2.{i}.beta"])
+        x = layer_norm(x + y, w[f"encoder.norm_layers_2.{i}.gamma"].reshape(1, -1, 1),
+                       w[f"encoder.norm_layers_2.{i}.beta"].reshape(1, -1, 1), eps_tf)
     x = x * x_mask
     x_m = F.conv1d(x, w["proj_m.weight"], w["proj_m.bias"]) * x_mask
     if mean_only:

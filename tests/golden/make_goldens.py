@@ -443,6 +443,14 @@ def main_glow_enc_types():
     ]
     for i, (name, cfg) in enumerate(cases):
         glow_encoder_case(Encoder, name, cfg, seed=301 + i, B=3, T=37, lengths=[37, 29, 13], tok_seed=51 + i)
+    # rel_pos_transformer with LayerNorm2 (layer_norm_type "2") and block-limited attention
+    # (input_length 3, transformer.py:148-150) beside relative embeddings (window 4)
+    lcfg = dict(base, encoder_type="rel_pos_transformer", mean_only=False, use_prenet=True,
+                encoder_params={"kernel_size": 3, "dropout_p": 0.1, "num_layers": 2, "num_heads": 2,
+                                "hidden_channels_ffn": 128, "rel_attn_window_size": 4, "input_length": 3,
+                                "layer_norm_type": "2"})
+    glow_encoder_case(Encoder, "glow_encoder_ln2_band_b3_t37", lcfg, seed=311, B=3, T=37, lengths=[37, 29, 13],
+                      tok_seed=61)
 
 
 def main_glow_tts_spk():

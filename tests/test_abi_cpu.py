@@ -388,6 +388,27 @@ def test_glow_encoder_other_types_inventory(et, ep, pre, nw):
     assert sum(w.size for w in ws) == sum(v.numel() for v in sd.values()) - tracked
 
 
+def test_glow_encoder_layernorm2_and_input_length_surface():
+    """layer_norm_type "2" (LayerNorm2: gamma / beta [C], transformer.py:386-387) and input_length
+    (block-limited attention, :148-150) reach the C-ABI configuration."""
+    from tts_amd.tts import Encoder
+
+    ep = {"kernel_size": 3, "dropout_p": 0.1, "num_layers": 2, "num_heads": 2, "hidden_channels_ffn": 128,
+          "rel_attn_window_size": 4, "input_length": 0, "layer_norm_type": "2"}
+    sd = synthetic.glow_encoder_state_dict(num_chars=30, out_channels=16, hidden_channels=64, hidden_channels_dp=48,
+                                           encoder_params=ep, mean_only=False, use_prenet=True, seed=4)
+    assert sd["encoder.norm_layers_1.0.gamma"].shape == (64,)
+    e = Encoder(30, 16, 64, 48, "rel_pos_transformer", ep, mean_only=False, use_prenet=True)
+    e.load_state_dict(sd)
+    assert (e._cfg.layer_norm_type, e._cfg.has_input_length, e._cfg.input_length) == (2, 1, 0)
+    ws = e._weight_list()
+    assert len(ws) == N.lib().tts_glow_encoder_num_weights(ctypes.byref(e._cfg))
+    for i, w in enumerate(ws):
+        assert N.lib().tts_glow_encoder_weight_numel(ctypes.byref(e._cfg), i) == w.size
+    with pytest.raises(ValueError, match="Unknown layer norm type"):
+        Encoder(30, 16, 64, 48, "rel_pos_transformer", dict(ep, layer_norm_type="3"))
+
+
 def test_glow_encoder_types_and_cpu_raise():
     from tts_amd.tts import Encoder, GlowTTS
 

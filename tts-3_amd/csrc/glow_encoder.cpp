@@ -111,6 +111,8 @@ void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
     TTS_REQUIRE(kset(c.kernel_size), 3, "FFN kernel_size must be 1, 3, 5, 7 or 11");
   }
   TTS_REQUIRE(c.rel_attn_window_size >= 0, 1, "rel_attn_window_size must be >= 0 (0 = None)");
+  TTS_REQUIRE(c.layer_norm_type >= 0 && c.layer_norm_type <= 2, 1, " [!] Unknown layer norm type");
+  TTS_REQUIRE(!c.has_input_length || c.input_length >= 0, 1, "input_length must be >= 0");
   TTS_REQUIRE(c.c_in_channels >= 0, 1, "c_in_channels must be >= 0");
   TTS_REQUIRE(c.math_mode >= MATH_FP32 && c.math_mode <= MATH_LAST, 1, "unknown math_mode");
   TTS_REQUIRE(c.math_mode != MATH_FP32_F16X3, 3,
@@ -343,10 +345,14 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
     run(prof, s, name, 2.0 * P * cv.Cout * cv.Cin * cv.K, 4.0 * P * (cv.Cin + cv.Cout + (res ? cv.Cout : 0)),
         [&] { launch_conv(mode, a, B, cv.K, cv.tile, s); });
   };
-  auto norm = [&](const char* name, const Norm& n, const float* a, const float* r, float* y, int C, bool relu) {
+  auto norm = [&](const char* name, const Norm& n, const float* a, const float* r, float* y, int C, bool relu,
+                  float eps = kEps) {
     run(prof, s, name, 0.0, 4.0 * P * C * (r ? 3 : 2),
-        [&] { launch_layernorm(a, r, n.gamma, n.beta, mask, y, B, C, T, kEps, relu, s); });
+        [&] { launch_layernorm(a, r, n.gamma, n.beta, mask, y, B, C, T, eps, relu, s); });
   };
+  // the transformer's own LayerNorms: LayerNorm2 (layer_norm_type "2") is F.layer_norm, eps 1e-5
+  // (normalization.py:42-53), the same normalisation with another eps
+  const float eps_tf = cfg_.layer_norm_type == 2 ? 1e-5f : kEps;
 
   // emb(x) * sqrt(H), transpose, x_mask (encoder.py:162-164)
   const float scale = (float)std::sqrt((double)H);
@@ -421,13 +427,14 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
     float* other = (x == X0) ? X1 : X0;
     conv("enc_qkv", L.qkv, x, Wd, nullptr, nullptr, 1.f, false);
     run(prof, s, "enc_attention", 4.0 * (double)B * T * T * H, 4.0 * P * 4 * H, [&] {
-      launch_attention(Wd, mask, L.ek, L.ev, A, B, H, cfg_.num_heads, T, cfg_.rel_attn_window_size, s);
+      launch_attention(Wd, mask, L.ek, L.ev, A, B, H, cfg_.num_heads, T, cfg_.rel_attn_window_size, s,
+                       cfg_.has_input_length ? cfg_.input_length : -1);
     });
     conv("enc_attn_o", L.o, A, other, x, nullptr, 1.f, false);          // x + conv_o(attn)
-    norm("enc_layernorm", L.n1, other, nullptr, other, H, false);         // norm_layers_1, * mask
+    norm("enc_layernorm", L.n1, other, nullptr, other, H, false, eps_tf);  // norm_layers_1, * mask
     conv("enc_ffn1", L.ffn1, other, Wd, nullptr, mask, 0.f, false);      // relu(conv_1(x*mask)) * mask
     conv("enc_ffn2", L.ffn2, Wd, x, other, mask, 1.f, false);            // x + conv_2(h*mask)*mask
-    norm("enc_layernorm", L.n2, x, nullptr, x, H, false);                 // norm_layers_2, * mask
+    norm("enc_layernorm", L.n2, x, nullptr, x, H, false, eps_tf);          // norm_layers_2, * mask
   }
   // heads (encoder.py:171-178)
   conv("enc_proj_m", proj_m_, x, x_m, nullptr, mask, 1.f, false);

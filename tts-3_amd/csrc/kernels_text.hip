@@ -261,7 +261,7 @@ void launch_glu_dw_swish(const float* a, const float* w, const float* bias, floa
 // Relative-position multi-head self-attention (transformer.py:142-180), one workgroup per
 // (8 queries, head, utterance):
 //   s[i][j] = (q_i . k_j) / sqrt(dk) + [|j-i| <= W] (q_i . ek[j-i+W]) / sqrt(dk)
-//   s = mask_i * mask_j ? s : -1e4;  p = softmax_j(s)
+//   s = mask_i * mask_j [* |j-i| <= input_length] ? s : -1e4;  p = softmax_j(s)
 //   o_i = sum_j p[i][j] v_j + sum_{|j-i| <= W} p[i][j] ev[j-i+W]
 // qkv: [B][3H][T] (rows q | k | v, head h = channels h*dk .. h*dk+dk-1), out: [B][H][T].
 // LDS: Q [8][dk], a K / V chunk [dk][64+1] (pad: conflict-free column reads), the 8 score
@@ -273,7 +273,8 @@ constexpr int ATT_MAX_DK = 128;
 
 __global__ void __launch_bounds__(256) attention_kernel(const float* __restrict__ qkv, const float* __restrict__ mask,
                                                         const float* __restrict__ ek, const float* __restrict__ ev,
-                                                        float* __restrict__ out, int H, int dk, int T, int W) {
+                                                        float* __restrict__ out, int H, int dk, int T, int W,
+                                                        int band) {
   extern __shared__ float lds[];
   float* Qs = lds;                             // [ATT_QB][dk]
   float* Kc = Qs + ATT_QB * ATT_MAX_DK;        // [dk][ATT_KC + 1]
@@ -339,7 +340,9 @@ __global__ void __launch_bounds__(256) attention_kernel(const float* __restrict_
     float* Sr = S + row * T;
     float mx = -INFINITY;
     for (int j = lane; j < T; j += 64) {
-      const float sv = (mi != 0.f && mb[j] != 0.f) ? Sr[j] : -1e4f;
+      // band >= 0: input_length's block mask (transformer.py:148-150), -1e4 outside |j - i| <= band
+      const bool in_band = band < 0 || (j - i <= band && i - j <= band);
+      const float sv = (mi != 0.f && mb[j] != 0.f && in_band) ? Sr[j] : -1e4f;
       Sr[j] = sv;
       mx = fmaxf(mx, sv);
     }
@@ -404,7 +407,7 @@ size_t attention_lds_bytes(int T) {
 }
 
 void launch_attention(const float* qkv, const float* mask, const float* ek, const float* ev, float* out, int B,
-                      int H, int heads, int T, int W, hipStream_t s) {
+                      int H, int heads, int T, int W, hipStream_t s, int band) {
   const int dk = H / heads;
   TTS_REQUIRE(dk >= 1 && dk <= ATT_MAX_DK && dk * heads == H, 3, "attention: head size must be <= 128");
   TTS_REQUIRE(T <= ATTN_MAX_T, 3, "attention: more than " + std::to_string(ATTN_MAX_T) + " tokens");
@@ -419,7 +422,7 @@ void launch_attention(const float* qkv, const float* mask, const float* ek, cons
   }
   dim3 grid(ceil_div(T, ATT_QB), heads, B);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), lds, s, qkv, mask, W > 0 ? ek : nullptr,
-                     W > 0 ? ev : nullptr, out, H, dk, T, W);
+                     W > 0 ? ev : nullptr, out, H, dk, T, W, band);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

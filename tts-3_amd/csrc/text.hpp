@@ -35,8 +35,9 @@ void launch_bn_act(const float* a, const float* scale, const float* shift, const
 void launch_glu_dw_swish(const float* a, const float* w, const float* bias, float* y, int B, int C, int T, int k,
                          hipStream_t s);
 // out[B][H][T] = multi-head attention of qkv [B][3H][T] (W = 0: no relative embeddings)
+// band >= 0: scores with |j - i| > band are -1e4 (input_length, transformer.py:148-150); -1: none
 void launch_attention(const float* qkv, const float* mask, const float* ek, const float* ev, float* out, int B,
-                      int H, int heads, int T, int W, hipStream_t s);
+                      int H, int heads, int T, int W, hipStream_t s, int band = -1);
 // xdp[b][c][t] = (c < H ? x[b][c][t] : g[b][c - H]) * mask[b][t]: the speaker-conditioned duration
 // predictor's input cat(x, g.expand(T)) (encoder.py:166-168, masked at duration_predictor.py:66)
 void launch_dp_input(const float* x, const float* g, const float* mask, float* xdp, int B, int H, int Cg, int T,

@@ -105,6 +105,9 @@ class TtsGlowEncoderCfg(Structure):
         ("num_conv_blocks", c_int),
         ("num_res_blocks", c_int),
         ("dilations", c_int * 32),
+        ("layer_norm_type", c_int),
+        ("has_input_length", c_int),
+        ("input_length", c_int),
     ]
 
 

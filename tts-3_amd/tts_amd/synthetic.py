@@ -366,6 +366,12 @@ def glow_encoder_state_dict(
     F_ = ep["hidden_channels_ffn"]
     nh = ep["num_heads"]
     W = ep.get("rel_attn_window_size")
+
+    def tnorm(name: str, c: int):  # the transformer's LayerNorm ("1", [1, C, 1]) or LayerNorm2 ("2", [C])
+        norm(name, c)
+        if ep.get("layer_norm_type", "1") == "2":
+            for k in ("gamma", "beta"):
+                sd[f"{name}.{k}"] = sd[f"{name}.{k}"].reshape(-1)
     if use_prenet:
         prenet_rcln()
     for l in range(ep["num_layers"]):
@@ -377,12 +383,12 @@ def glow_encoder_state_dict(
             sd[f"{pre}.emb_rel_k"] = t(rng.standard_normal((1, 2 * W + 1, kc)) * kc**-0.5)
             sd[f"{pre}.emb_rel_v"] = t(rng.standard_normal((1, 2 * W + 1, kc)) * kc**-0.5)
     for l in range(ep["num_layers"]):
-        norm(f"encoder.norm_layers_1.{l}", H)
+        tnorm(f"encoder.norm_layers_1.{l}", H)
     for l in range(ep["num_layers"]):
         conv(f"encoder.ffn_layers.{l}.conv_1", F_, H, K, 1.4)  # relu halves the variance
         conv(f"encoder.ffn_layers.{l}.conv_2", H, F_, K)
     for l in range(ep["num_layers"]):
-        norm(f"encoder.norm_layers_2.{l}", H)
+        tnorm(f"encoder.norm_layers_2.{l}", H)
     _glow_encoder_heads(sd, conv, norm, t, H, out_channels, hidden_channels_dp, mean_only, c_in_channels,
                         log_duration)
     return sd

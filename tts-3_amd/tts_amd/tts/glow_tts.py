@@ -44,6 +44,17 @@ class LayerNorm(nn.Module):
         self.beta = nn.Parameter(torch.zeros(1, channels, 1))
 
 
+class LayerNorm2(nn.Module):
+    """normalization.py:31-53 (parameters only): F.layer_norm over the channels, eps 1e-5."""
+
+    def __init__(self, channels: int, eps: float = 1e-5):
+        super().__init__()
+        self.channels = channels
+        self.eps = eps
+        self.gamma = nn.Parameter(torch.ones(channels))
+        self.beta = nn.Parameter(torch.zeros(channels))
+
+
 class ResidualConv1dLayerNormBlock(nn.Module):
     """glow.py:11-67 (parameters only)."""
 
@@ -68,6 +79,7 @@ class RelativePositionMultiHeadAttention(nn.Module):
         assert channels % num_heads == 0, " [!] channels should be divisible by num_heads."
         self.num_heads = num_heads
         self.rel_attn_window_size = rel_attn_window_size
+        self.input_length = input_length
         self.k_channels = channels // num_heads
         self.conv_q = nn.Conv1d(channels, channels, 1)
         self.conv_k = nn.Conv1d(channels, channels, 1)
@@ -95,10 +107,10 @@ class RelativePositionTransformer(nn.Module):
     def __init__(self, in_channels, out_channels, hidden_channels, hidden_channels_ffn, num_heads, num_layers,
                  kernel_size=1, dropout_p=0.0, rel_attn_window_size=None, input_length=None, layer_norm_type="1"):
         super().__init__()
-        if layer_norm_type != "1":
-            raise NotImplementedError("layer_norm_type '2' (LayerNorm2) is not implemented on the MI355X path")
-        if input_length is not None:
-            raise NotImplementedError("input_length (block-limited attention) is not implemented on the MI355X path")
+        if layer_norm_type not in ("1", "2"):
+            raise ValueError(" [!] Unknown layer norm type")  # transformer.py:388-389
+        self.layer_norm_type = layer_norm_type
+        self.input_length = input_length
         self.num_layers = num_layers
         self.attn_layers = nn.ModuleList()
         self.norm_layers_1 = nn.ModuleList()
@@ -107,12 +119,13 @@ class RelativePositionTransformer(nn.Module):
         for idx in range(num_layers):
             self.attn_layers.append(RelativePositionMultiHeadAttention(
                 hidden_channels if idx != 0 else in_channels, hidden_channels, num_heads,
-                rel_attn_window_size=rel_attn_window_size, dropout_p=dropout_p))
-            self.norm_layers_1.append(LayerNorm(hidden_channels))
+                rel_attn_window_size=rel_attn_window_size, dropout_p=dropout_p, input_length=input_length))
+            Norm = LayerNorm if layer_norm_type == "1" else LayerNorm2
+            self.norm_layers_1.append(Norm(hidden_channels))
             last = (idx + 1) == num_layers
             self.ffn_layers.append(FeedForwardNetwork(hidden_channels, out_channels if last else hidden_channels,
                                                       hidden_channels_ffn, kernel_size, dropout_p=dropout_p))
-            self.norm_layers_2.append(LayerNorm(out_channels if last else hidden_channels))
+            self.norm_layers_2.append(Norm(out_channels if last else hidden_channels))
 
 
 class GatedConvBlock(nn.Module):
@@ -272,6 +285,9 @@ class Encoder(nn.Module):
             c.num_heads = ep["num_heads"]
             c.num_layers = ep["num_layers"]
             c.rel_attn_window_size = ep.get("rel_attn_window_size") or 0
+            c.layer_norm_type = 2 if self.encoder.layer_norm_type == "2" else 1
+            if self.encoder.input_length is not None:
+                c.has_input_length, c.input_length = 1, int(self.encoder.input_length)
         elif et == "residual_conv_bn":
             d = self.encoder.dilations
             if len(d) > 32:
