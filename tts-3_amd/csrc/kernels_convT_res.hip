@@ -72,8 +72,11 @@ __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
   const int wr = wave % WR, wc = wave / WR;
   const int half = lane >> 5;
   const int l32 = lane & 31;
-  const int rs = RS > 1 ? (int)blockIdx.y : 0;
-  const int b = blockIdx.z;
+  // grid (tiles, B, RS): the pass share varies slowest, so the workgroups resident at one time
+  // mostly read one share's weights (2 MB at 512 channels, inside an XCD's 4 MB L2; the whole 8.4 MB
+  // set would not be)
+  const int rs = RS > 1 ? (int)blockIdx.z : 0;
+  const int b = blockIdx.y;
   const int t0 = blockIdx.x * P::BN;  // first frame (column) of the tile
   const int Tin = a.Tin;
   const int Cin = a.Cin;
@@ -208,7 +211,7 @@ template <class S, int NG, int WR, int TN, int RS = 1>
 void launch_res_t(const Conv1dArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.Cin == 16 * NG && a.Cout % (32 * WR) == 0 && a.Cout / (32 * WR) >= RS, 1,
               "convT_res: bad shape for this instance");
-  const dim3 grid(ceil_div(a.Tout, ConvTResCfg<S, NG, WR, TN>::BN), RS, B);
+  const dim3 grid(ceil_div(a.Tout, ConvTResCfg<S, NG, WR, TN>::BN), B, RS);
   hipLaunchKernelGGL((convT_res_kernel<S, NG, WR, TN, RS>), grid, dim3(512), 0, s, a);
 }
 // 256-row passes (8 row-block waves, 64-frame windows)
