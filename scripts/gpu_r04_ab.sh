@@ -12,7 +12,7 @@ if [ -z "$AB_SKIP_TESTS" ]; then
 fi
 B="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits"
 VARS=${AB_VARIANTS:-base new}
-for r in 1 2; do
+for r in $(seq 1 ${AB_ROUNDS:-2}); do
   for v in $VARS; do
     lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so; [ $v != new ] && lib=ab/lib_$v.so
     TTS_MI355X_LIB=$lib timeout -k 10 200 python $B > gpurun_out/ab_${v}_$r.json 2> gpurun_out/ab_${v}_$r.err || { tail -5 gpurun_out/ab_${v}_$r.err; exit 1; }

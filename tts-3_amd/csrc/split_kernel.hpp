@@ -20,6 +20,10 @@ struct SplitCfg {
   static_assert(XSZB % 16 == 0, "");
 };
 
+#ifndef SPLIT_STAGE_8R
+#define SPLIT_STAGE_8R 1  // staging lane map (see conv1d_split_kernel); 0: 4 rows x 4 quads per 16 lanes
+#endif
+
 #ifndef X6_ABLATE
 #define X6_ABLATE 0  // ablation builds (scripts/gpu_ablate.sh): 1 no staging refill, 2 no A stream
 #endif
@@ -133,14 +137,18 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
   const unsigned chb = (unsigned)Tin * 4u;  // bytes per channel row
 
-  // staging units (chunk invariant): unit u -> channel quad q, row r, group g
+  // staging units (chunk invariant): unit u -> channel quad q, row r, group g.  SPLIT_STAGE_8R: a
+  // 16-lane store group writes 8 consecutive rows x 2 quad positions; the row pitches (80 / 112 /
+  // 48 B) put 8 consecutive rows on 8 distinct 16-B slots of the 128-B bank row, so the group's
+  // 8-byte ds_write_b64 hit 32 distinct banks (4 rows x 4 quads: 2-way on half the groups), and a
+  // load instruction reads 32 contiguous bytes per channel instead of 16
   unsigned uvoff[C::UPT];  // byte offset of channel (16g+4q) at the clamped source time, or OOB
   int ulds[C::UPT];        // LDS offset of the row's quad
 #pragma unroll
   for (int i = 0; i < C::UPT; ++i) {
     const int u = tid + i * 256;
-    const int q = u & 3;
-    const int rr = u >> 2;
+    const int q = SPLIT_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
+    const int rr = SPLIT_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
     const int g = rr / XW;
     const int r = rr - g * XW;
     const int ts = t0 - a.pad + r;

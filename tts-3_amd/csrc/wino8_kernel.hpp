@@ -74,17 +74,21 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   constexpr int NP = S::NP;
   constexpr int NCH = C::NCH;
   constexpr bool H3 = S::SCALED;
+// weight prefetch depths (steps) of the two point groups and the transform-piece read->math gap
+// (steps) per kernel size; round-4 re-tune after the conflict-free job reads (3 rounds x 3 builds,
+// one box session): PD 3 / PD1 4 / GAP11 1 gave 53.5 ms per batch against 53.9 for the round-3
+// values 2 / 6 / 0 (PD 3 alone or GAP11 1 alone: 53.7; PD1 8 spills; GAP7 0: 54.1)
 #ifndef WINO8_PD
-#define WINO8_PD 2
+#define WINO8_PD 3
 #endif
 #ifndef WINO8_PD1
-#define WINO8_PD1 6
+#define WINO8_PD1 4
 #endif
 #ifndef WINO8_GAP7
 #define WINO8_GAP7 1
 #endif
 #ifndef WINO8_GAP11
-#define WINO8_GAP11 0
+#define WINO8_GAP11 1
 #endif
   __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
   __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
