@@ -28,6 +28,10 @@ namespace tts {
 //   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
 //   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
 //   instead of 92 KB); the halo costs (K - 1) / 192 of the columns instead of (K - 1) / 256.
+#ifndef RES_STAGE_8R
+#define RES_STAGE_8R 1  // x staging lane map of the pair / whole-block kernels (0: 4 rows x 4 quads)
+#endif
+
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false>
 struct PairCfg {
   static constexpr int RP_W = GEO == 0 ? 256 : 192;
@@ -94,8 +98,9 @@ void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
   for (int i = 0; i < P::UPT; ++i) {
     const int u = tid + i * 256;
-    const int q = u & 3;
-    const int r = u >> 2;
+    // RES_STAGE_8R: 8 rows x 2 quad positions per 16-lane store group (see conv1d_split_kernel)
+    const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
+    const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
     const int ts = tx0 - a1.pad + r;
     const bool ok = r < XW && ts >= 0 && ts < T;
     uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
@@ -469,8 +474,8 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
         const int u = tid + i * NT;
-        const int q = u & 3;
-        const int r = u >> 2;
+        const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
+        const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
         const int ts = tx0 - R3_XOFF + r;
         const bool ok = r < PR && ts >= 0 && ts < T;
         const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
@@ -499,8 +504,8 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
       for (int i = 0; i < UG; ++i) {
         const int u = tid + i * NT;
-        const int q = u & 3;
-        const int r = u >> 2;
+        const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
+        const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
         if (r < PR) {
           float v[4];
 #pragma unroll
