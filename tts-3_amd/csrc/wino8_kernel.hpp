@@ -81,6 +81,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_PD
 #define WINO8_PD 3
 #endif
+#ifndef WINO8_EARLY_W
+#define WINO8_EARLY_W 0
+#endif
 #ifndef WINO8_PD1
 #define WINO8_PD1 4
 #endif
@@ -226,31 +229,35 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       bpre = bpre + cv;  // the sum the two range-checked epilogue loads gave
     }
   }
-  // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0
+  // prologue: raw(0), raw(1) -> R0, R1; transform raw(0) -> T0.  With WINO8_EARLY_W the transform
+  // runs inside run() after the first weight prefetch is issued, so those loads overlap it; WL is
+  // the number of weight loads a wave has issued after its DMAs
   if (grp == 1) {
     dma(0, 0);
-    if (nc > 1) {
-      dma(1, 1);
+    if (nc > 1) dma(1, 1);
+  }
+  auto prologue = [&](auto wl_tag) {
+    constexpr int WL = decltype(wl_tag)::value;
+    if (grp == 1) {
       // raw(0) only: a wave issues at least NDMA / 4 instructions of raw(1) after it (in order)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NDMA / 4) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (nc > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::NDMA / 4 + WL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WL) : "memory");
     }
-  }
-  WSTAMP(1);
-  if (tid < 128) wbias[tid] = bpre;
-  lds_sync();
+    WSTAMP(1);
+    if (tid < 128) wbias[tid] = bpre;
+    lds_sync();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    job_load(0, j);
-    job_finish(0, j);
-  }
-  // raw(1) must have landed before the barrier: chunk 0's transform jobs read R[1] from its first
-  // step on.  No weight load is in flight yet, so this waits for the raw(1) DMA alone (it overlapped
-  // the chunk-0 transform above)
-  if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_sync();
-  WSTAMP(2);
+    for (int j = 0; j < 4; ++j) {
+      job_load(0, j);
+      job_finish(0, j);
+    }
+    // raw(1) must have landed before the barrier: chunk 0's transform jobs read R[1] from its first
+    // step on (this also waits for the prefetched weights, which overlapped the transform above)
+    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_sync();
+    WSTAMP(2);
+  };
+  if (!WINO8_EARLY_W) prologue(std::integral_constant<int, 0>{});
 
   // the chunk loop of one point group (NPG points starting at P0); both groups run it with the
   // same barrier sequence
@@ -275,6 +282,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     for (int v = 0; v < PD; ++v)
 #pragma unroll
       for (int q = 0; q < NP; ++q) ar[v][q] = bload4(ra, avoff, aoff(0, v) + (unsigned)q * 1024u);
+    if (WINO8_EARLY_W) prologue(std::integral_constant<int, PD * NP>{});
     auto read_b = [&](const unsigned char* tl, int v, f32x4 (*dst)[NP]) {
       const int p = P0 + v % NPG, c = v / NPG;
 #pragma unroll
