@@ -93,6 +93,9 @@ def parse():
                    help="utterances of the bench batch the CPU baseline vocodes (0: the whole batch)")
     p.add_argument("--vits-batch", type=int, default=64, help="config 5 global batch (N > 1 leg)")
     p.add_argument("--vits-frames", type=int, default=1024, help="config 5 latent frames per utterance")
+    p.add_argument("--vits-math-mode", default="bf16", choices=sorted(MODE_PEAK),
+                   help="arithmetic of the config-5 sharded leg (BASELINE.json configs[4] names bf16; "
+                        "independent of --math-mode, which sets the headline leg)")
     p.add_argument("--rehearse-sharded", action="store_true",
                    help="N = 1 only: run the config-4 / config-5 sharded legs over a one-rank process group "
                         "(exercises the RCCL scatter/gather path on one GPU; reported under *_rehearsal)")
@@ -722,7 +725,7 @@ def main():
         }
     if dist_on and not a.no_vits:  # config 5 at N > 1 (its N = 1 side line is vits_waveform)
         v5 = vits_sharded_bench(dev, world, rank, a.steps, a.warmup, stub=a.stub, global_batch=a.vits_batch,
-                                T=a.vits_frames)
+                                T=a.vits_frames, mode=a.vits_math_mode)
         if rank == 0:
             rec["config5_sharded_rehearsal" if rehearse else "config5_sharded"] = v5
     if a.stub:

@@ -310,6 +310,30 @@ BENCH_ORACLE_ROWS = (0, 9, 17, 31)
 
 
 @functools.lru_cache(maxsize=None)
+def _config1_case():
+    sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
+    mel = synthetic.mel(1, 256, seed=0)
+    return sd, mel, hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_config1_single_mel_vs_oracle(cuda_device, mode):
+    """BASELINE.json configs[0]: HiFiGAN-v1 on one 80 x 256 mel through the drop-in
+    ``HifiganGenerator.inference`` (hifigan_generator.py:267-282, replicate pad 5), here on the HIP
+    path in every math mode against the fp64 oracle.  (The reference runs this config on the CPU;
+    the product has no CPU path by design, so the CPU side of config 1 is the oracle itself.)"""
+    sd, mel, ref = _config1_case()
+    g = HifiganGenerator(**V1, math_mode=mode)
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    out = g.inference(mel.to(cuda_device))
+    assert out.shape == (1, 1, 256 * 266)
+    assert torch.isfinite(out).all() and out.abs().max() <= 1.0
+    assert_close_fp32(out.cpu(), ref, f"config 1 [1,80,256] ({mode})", **tol(mode))
+
+
+@functools.lru_cache(maxsize=None)
 def _bench_row_oracle(i):
     sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
     mel = synthetic.mel(32, 1024, seed=0)[i : i + 1]

@@ -6,11 +6,14 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 
 namespace tts {
 
-// log(det(W)) of an S x S matrix in fp64 (partial-pivot LU); the InvConvNear weight has det > 0
-// (glow.py:94-95); a non-positive determinant is rejected like torch.logdet's NaN / -inf
+// log(det(W)) of an S x S matrix in fp64 (partial-pivot LU).  The InvConvNear weight is born with
+// det > 0 (glow.py:94-95); otherwise this returns what torch.logdet gives (glow.py:128): -inf for a
+// singular matrix, NaN for a negative determinant.  Only the forward direction's logdet reads it, so a
+// checkpoint with such a weight still loads and runs reverse (the reference's inference path)
 double logdet_fp64(const float* w, int S) {
   std::vector<double> a((size_t)S * S);
   for (int i = 0; i < S * S; ++i) a[i] = w[i];
@@ -20,7 +23,7 @@ double logdet_fp64(const float* w, int S) {
     int p = k;
     for (int r = k + 1; r < S; ++r)
       if (std::fabs(a[(size_t)r * S + k]) > std::fabs(a[(size_t)p * S + k])) p = r;
-    if (a[(size_t)p * S + k] == 0.0) throw Error(1, "InvConvNear weight is singular");
+    if (a[(size_t)p * S + k] == 0.0) return -std::numeric_limits<double>::infinity();
     if (p != k) {
       for (int c = 0; c < S; ++c) std::swap(a[(size_t)p * S + c], a[(size_t)k * S + c]);
       sign = -sign;
@@ -33,8 +36,7 @@ double logdet_fp64(const float* w, int S) {
       for (int c = k; c < S; ++c) a[(size_t)r * S + c] -= f * a[(size_t)k * S + c];
     }
   }
-  TTS_REQUIRE(sign > 0, 1, "InvConvNear weight has a negative determinant (logdet undefined)");
-  return ld;
+  return sign > 0 ? ld : std::numeric_limits<double>::quiet_NaN();
 }
 
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil) {

@@ -315,7 +315,9 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
   TTS_REQUIRE(tok && len && x_m && logw && x_mask, 1, "NULL input/output pointer");
   TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1 && T >= 1, 1, "batch and token count must be >= 1");
-  TTS_REQUIRE(T <= ATTN_MAX_T, 3, "more than " + std::to_string(ATTN_MAX_T) + " tokens per utterance");
+  // the attention kernel keeps whole score rows in LDS; the convolutional encoder types have no such bound
+  TTS_REQUIRE(cfg_.encoder_type != TTS_ENC_REL_POS_TRANSFORMER || T <= ATTN_MAX_T, 3,
+              "more than " + std::to_string(ATTN_MAX_T) + " tokens per utterance (rel_pos_transformer)");
   DeviceGuard dg(device_);
   reserve(B, T);
   const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, D = cfg_.hidden_channels_dp;
