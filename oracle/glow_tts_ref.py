@@ -86,6 +86,33 @@ def rel_attention(q, k, v, mask, num_heads, emb_rel_k=None, emb_rel_v=None, inpu
     return out.transpose(2, 3).contiguous().view(b, c, t)
 
 
+def rel_transformer(w, x, x_mask, ep, prefix="encoder"):
+    """RelativePositionTransformer.forward (transformer.py:410-432) with in = out = hidden: per layer
+    x = LN1(x*mask + attn(x*mask)); x = LN2(x + FFN(x, mask)); LayerNorm2 (layer_norm_type "2",
+    normalization.py:42-53) is F.layer_norm over channels with eps 1e-5, LayerNorm ("1") eps 1e-4."""
+    K = ep.get("kernel_size", 1)
+    pl, pr = (K - 1) // 2, K // 2
+    eps_tf = 1e-5 if ep.get("layer_norm_type", "1") == "2" else 1e-4
+    for i in range(ep["num_layers"]):  # transformer.py:420-431
+        pre = f"{prefix}.attn_layers.{i}"
+        x = x * x_mask
+        q = F.conv1d(x, w[f"{pre}.conv_q.weight"], w[f"{pre}.conv_q.bias"])
+        k = F.conv1d(x, w[f"{pre}.conv_k.weight"], w[f"{pre}.conv_k.bias"])
+        v = F.conv1d(x, w[f"{pre}.conv_v.weight"], w[f"{pre}.conv_v.bias"])
+        a = rel_attention(q, k, v, x_mask, ep["num_heads"], w.get(f"{pre}.emb_rel_k"), w.get(f"{pre}.emb_rel_v"),
+                          ep.get("input_length"))
+        y = F.conv1d(a, w[f"{pre}.conv_o.weight"], w[f"{pre}.conv_o.bias"])
+        x = layer_norm(x + y, w[f"{prefix}.norm_layers_1.{i}.gamma"].reshape(1, -1, 1),
+                       w[f"{prefix}.norm_layers_1.{i}.beta"].reshape(1, -1, 1), eps_tf)
+        f = f"{prefix}.ffn_layers.{i}"
+        y = F.conv1d(F.pad(x * x_mask, [pl, pr]), w[f"{f}.conv_1.weight"], w[f"{f}.conv_1.bias"])
+        y = torch.relu(y)
+        y = F.conv1d(F.pad(y * x_mask, [pl, pr]), w[f"{f}.conv_2.weight"], w[f"{f}.conv_2.bias"]) * x_mask
+        x = layer_norm(x + y, w[f"{prefix}.norm_layers_2.{i}.gamma"].reshape(1, -1, 1),
+                       w[f"{prefix}.norm_layers_2.{i}.beta"].reshape(1, -1, 1), eps_tf)
+    return x
+
+
 def _bn(x, w, pre, eps=1e-5):
     """nn.BatchNorm1d in eval mode (running statistics)."""
     return F.batch_norm(x, w[f"{pre}.running_mean"], w[f"{pre}.running_var"], w[f"{pre}.weight"], w[f"{pre}.bias"],
@@ -150,25 +177,8 @@ def encoder_forward(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: 
             h = h * torch.sigmoid(h)
             h = _bn(F.conv1d(h, w[f"{pre}.time_conv2.weight"], w[f"{pre}.time_conv2.bias"]), w, f"{pre}.norm3")
             x = x + h
-    # LayerNorm2 (layer_norm_type "2", normalization.py:42-53): F.layer_norm, eps 1e-5
-    eps_tf = 1e-5 if ep.get("layer_norm_type", "1") == "2" else 1e-4
-    for i in range(ep["num_layers"] if et == "rel_pos_transformer" else 0):  # transformer.py:420-431
-        pre = f"encoder.attn_layers.{i}"
-        x = x * x_mask
-        q = F.conv1d(x, w[f"{pre}.conv_q.weight"], w[f"{pre}.conv_q.bias"])
-        k = F.conv1d(x, w[f"{pre}.conv_k.weight"], w[f"{pre}.conv_k.bias"])
-        v = F.conv1d(x, w[f"{pre}.conv_v.weight"], w[f"{pre}.conv_v.bias"])
-        a = rel_attention(q, k, v, x_mask, ep["num_heads"], w.get(f"{pre}.emb_rel_k"), w.get(f"{pre}.emb_rel_v"),
-                          ep.get("input_length"))
-        y = F.conv1d(a, w[f"{pre}.conv_o.weight"], w[f"{pre}.conv_o.bias"])
-        x = layer_norm(x + y, w[f"encoder.norm_layers_1.{i}.gamma"].reshape(1, -1, 1),
-                       w[f"encoder.norm_layers_1.{i}.beta"].reshape(1, -1, 1), eps_tf)
-        f = f"encoder.ffn_layers.{i}"
-        y = F.conv1d(F.pad(x * x_mask, [pl, pr]), w[f"{f}.conv_1.weight"], w[f"{f}.conv_1.bias"])
-        y = torch.relu(y)
-        y = F.conv1d(F.pad(y * x_mask, [pl, pr]), w[f"{f}.conv_2.weight"], w[f"{f}.conv_2.bias"]) * x_mask
-        x = layer_norm(x + y, w[f"encoder.norm_layers_2.{i}.gamma"].reshape(1, -1, 1),
-                       w[f"encoder.norm_layers_2.{i}.beta"].reshape(1, -1, 1), eps_tf)
+    if et == "rel_pos_transformer":
+        x = rel_transformer(w, x, x_mask, ep)
     x = x * x_mask
     x_m = F.conv1d(x, w["proj_m.weight"], w["proj_m.bias"]) * x_mask
     if mean_only:

@@ -6,6 +6,7 @@ the GPU box):   python tests/golden/make_goldens.py        (HiFiGAN + Glow fixtu
                 python tests/golden/make_goldens.py glow_tts (Glow-TTS encoder + inference glue)
                 python tests/golden/make_goldens.py glow_cond (speaker-conditioned Glow decoder)
                 python tests/golden/make_goldens.py glow_enc_types (gated / residual-BN / TDS encoders)
+                python tests/golden/make_goldens.py vits_text (Vits.inference: text encoder, SDP, glue)
 
 Import recipe: the hot-path leaf modules need only torch/fsspec/packaging,
 but ``TTS/vocoder/models/__init__.py`` and ``TTS/tts/layers/__init__.py`` import coqpit
@@ -328,6 +329,114 @@ def vits_posterior_case(PosteriorEncoder, name, cfg, seed, B, T, lengths, x_seed
           f"max|fp32-fp64| {np.abs(z32.numpy() - z64.numpy()).max():.2e}")
 
 
+def import_reference_vits_text():
+    HifiganGenerator, _ = import_reference()
+    from TTS.tts.layers.vits.networks import ResidualCouplingBlocks, TextEncoder
+    from TTS.tts.layers.vits.stochastic_duration_predictor import StochasticDurationPredictor
+    from TTS.tts.utils.helpers import generate_path, sequence_mask
+
+    return TextEncoder, StochasticDurationPredictor, ResidualCouplingBlocks, HifiganGenerator, generate_path, sequence_mask
+
+
+def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok_seed, gin=0):
+    """G14: Vits.inference (vits.py:1121-1162) tokens -> waveform through the reference's TextEncoder,
+    StochasticDurationPredictor(reverse=True), generate_path / sequence_mask, ResidualCouplingBlocks
+    and HifiganGenerator.  Vits itself imports torchaudio / librosa / coqpit (absent), so the glue's
+    lines are restated here around the reference modules.  Both noise draws (the SDP's torch.randn
+    at stochastic_duration_predictor.py:277 and randn_like(m_p) at vits.py:1154) are made here with
+    fixed seeds and stored; the fp64 run reuses them.  gin > 0: a speaker vector g [B, gin, 1] drawn
+    and stored, fed to the SDP (condition_dp_on_speaker), the flow and the decoder as vits.py does."""
+    TextEncoder, SDP, RCB, HifiganGenerator, generate_path, sequence_mask = refs
+    torch.manual_seed(0)
+    te = TextEncoder(tcfg["num_chars"], tcfg["out_channels"], tcfg["hidden_channels"], tcfg["hidden_channels_ffn"],
+                     tcfg["num_heads"], tcfg["num_layers"], tcfg["kernel_size"], 0.1)
+    te.load_state_dict(synthetic.vits_text_encoder_state_dict(**tcfg, seed=seeds[0]))
+    dp = SDP(scfg["in_channels"], scfg["hidden_channels"], scfg["kernel_size"], 0.5, scfg["num_flows"],
+             cond_channels=gin)
+    dp.load_state_dict(synthetic.vits_sdp_state_dict(**scfg, cond_channels=gin, seed=seeds[1]))
+    fl = RCB(fcfg["channels"], fcfg["hidden_channels"], fcfg["kernel_size"], fcfg["dilation_rate"], fcfg["num_layers"],
+             num_flows=fcfg["num_flows"], cond_channels=gin)
+    fl.load_state_dict(synthetic.vits_flow_state_dict(**dict(fcfg, cond_channels=gin), seed=seeds[2]))
+    dec = HifiganGenerator(**{k: v for k, v in dict(dcfg, cond_channels=gin).items() if k != "num_chars"})
+    dec.load_state_dict(synthetic.hifigan_state_dict(**dict(dcfg, cond_channels=gin), seed=seeds[3], weight_norm=True))
+    for m in (te, dp, fl, dec):
+        m.eval()
+    tok = synthetic.tokens(B, T, tcfg["num_chars"], seed=tok_seed)
+    lens = torch.tensor(lengths)
+    gen = torch.Generator().manual_seed(tok_seed + 300)
+    g = torch.randn(B, gin, 1, generator=gen) if gin else None
+    noise_dp = torch.randn(B, 2, T, generator=gen)
+    ns, ls, ns_dp = 0.667, 1.0, 1.0  # VitsArgs inference_noise_scale, length_scale, inference_noise_scale_dp
+
+    def infer(dtype, noise_z):
+        mods = [m.to(dtype) for m in (te, dp, fl, dec)]
+        gg = g.to(dtype) if g is not None else None
+        with torch.no_grad():
+            x, m_p, logs_p, x_mask = mods[0](tok, lens)
+            # the SDP's own draw replaced by the stored one (torch.randn(x.size(0), 2, x.size(2)))
+            orig = torch.randn
+            torch.randn = lambda *a, **k: noise_dp.clone()
+            try:
+                logw = mods[1](x, x_mask, g=gg, reverse=True, noise_scale=ns_dp)
+            finally:
+                torch.randn = orig
+            w = torch.exp(logw) * x_mask * ls
+            w_ceil = torch.ceil(w)
+            y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
+            y_mask = sequence_mask(y_lengths, None).to(x_mask.dtype).unsqueeze(1)
+            attn_mask = x_mask * y_mask.transpose(1, 2)
+            attn = generate_path(w_ceil.squeeze(1), attn_mask.squeeze(1).transpose(1, 2))
+            mp = torch.matmul(attn.transpose(1, 2), m_p.transpose(1, 2)).transpose(1, 2)
+            lp = torch.matmul(attn.transpose(1, 2), logs_p.transpose(1, 2)).transpose(1, 2)
+            if noise_z is None:
+                noise_z = torch.randn(mp.shape, generator=torch.Generator().manual_seed(tok_seed + 301))
+            z_p = mp + noise_z.to(dtype) * torch.exp(lp) * ns
+            z = mods[2](z_p, y_mask, g=gg, reverse=True)
+            wav = mods[3](z * y_mask, g=gg)
+        out = dict(x=x, m_p=m_p, logs_p=logs_p, x_mask=x_mask, logw=logw, w=w, w_ceil=w_ceil, y_lengths=y_lengths,
+                   y_mask=y_mask, attn=attn, m_p_exp=mp, logs_p_exp=lp, z_p=z_p, z=z, wav=wav)
+        return out, noise_z
+
+    o32, noise_z = infer(torch.float32, None)
+    o64, _ = infer(torch.float64, noise_z)
+    for k in ("w_ceil", "y_lengths"):
+        assert torch.equal(o32[k].double(), o64[k].double()), f"{k}: fp32 and fp64 reference disagree"
+    arrays = dict(tokens=tok.numpy(), lengths=lens.numpy(), noise_dp=noise_dp.numpy(), noise_z=noise_z.numpy())
+    if g is not None:
+        arrays["g"] = g.numpy()
+    for k, v in o32.items():
+        arrays[f"{k}_ref_fp32"] = v.numpy()
+    for k, v in o64.items():
+        arrays[f"{k}_ref_fp64"] = v.numpy()
+    wv = o64["w"][o64["x_mask"] > 0]
+    frac = (wv - torch.floor(wv)).numpy()
+    margin = float(np.minimum(frac, 1 - frac).min())
+    meta = dict(kind="vits_text", text_encoder=tcfg, sdp=scfg, flow=fcfg, decoder=dcfg, seeds=list(seeds),
+                tok_seed=tok_seed, B=B, T=T, lengths=lengths, gin=gin, noise_scale=ns, length_scale=ls,
+                noise_scale_dp=ns_dp, ceil_margin=margin)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, meta=json.dumps(meta), **arrays)
+    print(f"wrote {path}: y_lengths {o32['y_lengths'].tolist()} wav {tuple(o32['wav'].shape)} ceil margin "
+          f"{margin:.2e} max|fp32-fp64| logw {np.abs(arrays['logw_ref_fp32'] - arrays['logw_ref_fp64']).max():.2e} "
+          f"wav {np.abs(arrays['wav_ref_fp32'] - arrays['wav_ref_fp64']).max():.2e}")
+
+
+def main_vits_text():
+    refs = import_reference_vits_text()
+    from tts_amd.config import VITS_FLOW, VITS_SDP, VITS_TEXT_ENCODER
+
+    tcfg = dict(VITS_TEXT_ENCODER, num_chars=64)
+    dcfg = dict(in_channels=192, out_channels=1, resblock_type="1",
+                resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+                upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=128, upsample_factors=[8, 8, 2, 2],
+                inference_padding=0, conv_pre_weight_norm=False, conv_post_weight_norm=False, conv_post_bias=False)
+    fcfg = dict(VITS_FLOW, cond_channels=0)
+    vits_text_case(refs, "vits_text_b3_t13", tcfg, dict(VITS_SDP), fcfg, dcfg, (7531, 9753, 2470, 101), B=3, T=13,
+                   lengths=[13, 8, 1], tok_seed=51)
+    vits_text_case(refs, "vits_text_spk_b2_t11", tcfg, dict(VITS_SDP), fcfg, dcfg, (7532, 9754, 2471, 102), B=2,
+                   T=11, lengths=[11, 6], tok_seed=52, gin=16)
+
+
 def main_vits_posterior():
     PosteriorEncoder = import_reference_vits_posterior()
     from tts_amd.config import VITS_POSTERIOR
@@ -341,6 +450,8 @@ def main_vits_posterior():
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "vits_text":
+        return main_vits_text()
     if len(sys.argv) > 1 and sys.argv[1] == "vits_posterior":
         return main_vits_posterior()
     if len(sys.argv) > 1 and sys.argv[1] == "vits":

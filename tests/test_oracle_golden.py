@@ -280,3 +280,65 @@ def test_wav_int16_nonfinite_contract():
         assert handoff_ref.wav_int16(w).tolist() == [-50, 0, 20, 0, 3276, 0]  # scale 32767 / 0.01
         w = np.array([0.5, -0.2, -np.inf, 0.0], dtype=np.float32)  # max = inf: scale 0, inf * 0 = NaN
         assert handoff_ref.wav_int16(w).tolist() == [0, 0, 0, 0]
+
+
+VTEXT = goldens("vits_text")
+
+
+@pytest.mark.parametrize("name,meta,arr", VTEXT, ids=[g[0] for g in VTEXT])
+def test_vits_text_oracle_matches_reference(name, meta, arr):
+    """oracle/vits_text_ref.py against the reference's Vits.inference chain (make_goldens.py
+    vits_text): TextEncoder, SDP reverse with the stored noise, the duration glue, then the flow
+    and decoder oracles close it to the waveform (fp64 throughout)."""
+    from oracle import vits_text_ref
+
+    tcfg, scfg, gin = meta["text_encoder"], meta["sdp"], meta["gin"]
+    tsd = synthetic.vits_text_encoder_state_dict(**tcfg, seed=meta["seeds"][0])
+    tok, lens = torch.from_numpy(arr["tokens"]), torch.from_numpy(arr["lengths"])
+    x, m, logs, xm = vits_text_ref.text_encoder(tsd, tok, lens, dtype=torch.float64, **tcfg)
+    for n, o in (("x", x), ("m_p", m), ("logs_p", logs), ("x_mask", xm)):
+        assert max_abs(o.numpy(), arr[f"{n}_ref_fp64"]) < 1e-10, n
+    g = torch.from_numpy(arr["g"]).double() if gin else None
+    ssd = synthetic.vits_sdp_state_dict(**scfg, cond_channels=gin, seed=meta["seeds"][1])
+    logw = vits_text_ref.sdp_reverse(ssd, x, xm, torch.from_numpy(arr["noise_dp"]), g=g,
+                                     noise_scale=meta["noise_scale_dp"], dtype=torch.float64, **scfg)
+    assert max_abs(logw.numpy(), arr["logw_ref_fp64"]) < 1e-10
+    w_ceil, y_len = vits_text_ref.vits_durations(logw, xm, meta["length_scale"])
+    assert torch.equal(w_ceil, torch.from_numpy(arr["w_ceil_ref_fp64"]))
+    assert torch.equal(y_len, torch.from_numpy(arr["y_lengths_ref_fp64"]))
+    z_p, y_mask, mp, lp, attn = vits_text_ref.vits_expand(w_ceil, xm, y_len, m, logs, torch.from_numpy(arr["noise_z"]),
+                                                          meta["noise_scale"])
+    assert torch.equal(attn, torch.from_numpy(arr["attn_ref_fp64"]))
+    assert torch.equal(y_mask, torch.from_numpy(arr["y_mask_ref_fp64"]))
+    assert max_abs(mp.numpy(), arr["m_p_exp_ref_fp64"]) < 1e-12
+    assert max_abs(z_p.numpy(), arr["z_p_ref_fp64"]) < 1e-12
+    fcfg = dict(meta["flow"], cond_channels=gin)
+    fsd = synthetic.vits_flow_state_dict(**fcfg, seed=meta["seeds"][2])
+    z = vits_ref.vits_flow_reverse(fsd, z_p, y_mask, g=g, dtype=torch.float64, **fcfg)
+    assert max_abs(z.numpy(), arr["z_ref_fp64"]) < 1e-10
+    dcfg = dict(meta["decoder"], cond_channels=gin)
+    dsd = synthetic.hifigan_state_dict(**dcfg, seed=meta["seeds"][3], weight_norm=True)
+    wav = hifigan_ref.hifigan_forward(dsd, z * y_mask, pad=0, g=g, dtype=torch.float64, fold_dtype=torch.float64,
+                                      **dcfg)
+    assert max_abs(wav.numpy(), arr["wav_ref_fp64"]) < 1e-10
+    # fp32 oracle vs the reference's fp32 run, and the duration ceil() margin
+    x32, m32, _, _ = vits_text_ref.text_encoder(tsd, tok, lens, dtype=torch.float32, **tcfg)
+    assert max_abs(x32.numpy(), arr["x_ref_fp32"]) < 1e-4
+    assert meta["ceil_margin"] > 1e-3
+
+
+def test_rq_spline_inverse_roundtrip():
+    """The rational-quadratic spline restatement: forward then inverse returns the input inside the
+    tail bound and the identity outside it; log|det| of the two directions cancel."""
+    from oracle import vits_text_ref
+
+    gen = torch.Generator().manual_seed(5)
+    x = torch.linspace(-6, 6, 97, dtype=torch.float64)
+    uw, uh = torch.randn(97, 10, generator=gen).double(), torch.randn(97, 10, generator=gen).double()
+    ud = torch.randn(97, 9, generator=gen).double()
+    y, l1 = vits_text_ref.rq_spline(x, uw, uh, ud, False, 5.0)
+    x2, l2 = vits_text_ref.rq_spline(y, uw, uh, ud, True, 5.0)
+    assert max_abs(x2.numpy(), x.numpy()) < 1e-12
+    assert max_abs((l1 + l2).numpy(), np.zeros(97)) < 1e-12
+    out = (x.abs() > 5.0)
+    assert torch.equal(y[out], x[out])

@@ -7,6 +7,8 @@ JSON reader (no coqpit dependency).
   ``GlowTTS.__init__`` hands them to ``Encoder`` (TTS/tts/models/glow_tts.py:80-91)
 * ``VITS_FLOW`` / ``VITS_DECODER``: the flow and waveform-decoder fields of ``VitsArgs``
   (TTS/tts/models/vits.py:545-565, built at :675-682 and :704-718)
+* ``VITS_TEXT_ENCODER`` / ``VITS_SDP`` / ``VITS_INFERENCE``: the text side of ``Vits.inference``
+  (vits.py:653-692, :1088-1174)
 """
 from __future__ import annotations
 
@@ -71,6 +73,23 @@ VITS_POSTERIOR: Dict[str, Any] = {
     "dilation_rate": 1,         # dilation_rate_posterior_encoder
     "num_layers": 16,           # num_layers_posterior_encoder
 }
+
+# TextEncoder of VitsArgs (vits.py:653-663; networks.py:29-81): n_vocab = num_chars,
+# out = hidden = hidden_channels
+VITS_TEXT_ENCODER: Dict[str, Any] = {
+    "out_channels": 192,        # hidden_channels
+    "hidden_channels": 192,
+    "hidden_channels_ffn": 768,  # hidden_channels_ffn_text_encoder
+    "num_heads": 2,             # num_heads_text_encoder
+    "num_layers": 6,            # num_layers_text_encoder
+    "kernel_size": 3,           # kernel_size_text_encoder
+}
+
+# StochasticDurationPredictor of VitsArgs (vits.py:684-692): in = hidden_channels, 192 hidden, k3, 4 flows
+VITS_SDP: Dict[str, Any] = {"in_channels": 192, "hidden_channels": 192, "kernel_size": 3, "num_flows": 4}
+
+# Vits.inference scalars (VitsArgs, vits.py:569-572)
+VITS_INFERENCE: Dict[str, Any] = {"inference_noise_scale": 0.667, "length_scale": 1.0, "inference_noise_scale_dp": 1.0}
 
 VITS_DECODER: Dict[str, Any] = {
     "in_channels": 192,

@@ -23,7 +23,7 @@ from typing import Dict, List, Sequence
 import numpy as np
 import torch
 
-from .config import HIFIGAN_V1, GLOW_TTS_DECODER, GLOW_TTS_ENCODER, VITS_FLOW
+from .config import HIFIGAN_V1, GLOW_TTS_DECODER, GLOW_TTS_ENCODER, VITS_FLOW, VITS_SDP, VITS_TEXT_ENCODER
 
 
 def _wn_pair(rng, v: np.ndarray):
@@ -406,6 +406,106 @@ def _glow_encoder_heads(sd, conv, norm, t, H, out_channels, hidden_channels_dp, 
     norm("duration_predictor.norm_2", hidden_channels_dp)
     conv("duration_predictor.proj", 1, hidden_channels_dp, 1, 0.3)
     sd["duration_predictor.proj.bias"] = t(np.full((1,), log_duration))
+
+
+def vits_text_encoder_state_dict(
+    num_chars: int = 64,
+    out_channels: int = VITS_TEXT_ENCODER["out_channels"],
+    hidden_channels: int = VITS_TEXT_ENCODER["hidden_channels"],
+    hidden_channels_ffn: int = VITS_TEXT_ENCODER["hidden_channels_ffn"],
+    num_heads: int = VITS_TEXT_ENCODER["num_heads"],
+    num_layers: int = VITS_TEXT_ENCODER["num_layers"],
+    kernel_size: int = VITS_TEXT_ENCODER["kernel_size"],
+    seed: int = 7531,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a VITS ``TextEncoder`` (TTS/tts/layers/vits/networks.py:29-81): the
+    RelativePositionTransformer keys of ``glow_encoder_state_dict`` (LayerNorm2, window 4) under
+    ``encoder.``, then ``proj`` (H -> 2 out); the log-scale rows of ``proj`` are drawn small so
+    exp(logs) stays O(1)."""
+    ep = dict(kernel_size=kernel_size, num_layers=num_layers, num_heads=num_heads,
+              hidden_channels_ffn=hidden_channels_ffn, rel_attn_window_size=4, layer_norm_type="2")
+    g = glow_encoder_state_dict(num_chars=num_chars, out_channels=out_channels, hidden_channels=hidden_channels,
+                                encoder_params=ep, mean_only=True, use_prenet=False, seed=seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict(
+        (k, v) for k, v in g.items() if k == "emb.weight" or k.startswith("encoder."))
+    rng = np.random.default_rng(seed + 1)
+    H = hidden_channels
+    w = rng.standard_normal((2 * out_channels, H, 1)) / np.sqrt(H)
+    w[out_channels:] *= 0.3
+    sd["proj.weight"] = torch.from_numpy(w.astype(np.float32))
+    sd["proj.bias"] = torch.from_numpy((rng.standard_normal(2 * out_channels) * 0.02).astype(np.float32))
+    return sd
+
+
+def vits_sdp_state_dict(
+    in_channels: int = VITS_SDP["in_channels"],
+    hidden_channels: int = VITS_SDP["hidden_channels"],
+    kernel_size: int = VITS_SDP["kernel_size"],
+    num_flows: int = VITS_SDP["num_flows"],
+    cond_channels: int = 0,
+    seed: int = 9753,
+    log_duration: float = 1.6,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of a VITS ``StochasticDurationPredictor`` (stochastic_duration_predictor.py:
+    150-227), every key including the training-only posterior side (post_*).
+
+    * 1x1 convs variance-preserving, depthwise convs ~ N(0, 1/k), LayerNorm2 gamma ~ 1 + 0.1 N
+    * the ConvFlow ``proj`` (zero-initialised by the reference, an identity spline) ~ N(0, 0.5/H)
+      with widths / heights / derivatives of O(1) after the 1/sqrt(H) scaling
+    * ElementwiseAffine translation ~ -log_duration + 0.2 N on channel 0 (the logw channel at the
+      end of the reverse chain: logw = (z0 - t0) exp(-log_scale0)), log_scale ~ 0.1 N, so exp(logw)
+      is a few frames per token
+    """
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    H = hidden_channels
+    nb = 10
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+
+    def conv(name, cout, cin, k, scale=1.0, groups=1, bias_std=0.02):
+        sd[f"{name}.weight"] = t(rng.standard_normal((cout, cin // groups, k)) * (scale / np.sqrt(cin // groups * k)))
+        sd[f"{name}.bias"] = t(rng.standard_normal((cout,)) * bias_std)
+
+    def dds(pre):
+        for i in range(3):
+            conv(f"{pre}.convs_sep.{i}", H, H, kernel_size, groups=H)
+        for i in range(3):
+            conv(f"{pre}.convs_1x1.{i}", H, H, 1)
+        for n in ("norms_1", "norms_2"):
+            for i in range(3):
+                sd[f"{pre}.{n}.{i}.gamma"] = t(1.0 + 0.1 * rng.standard_normal(H))
+                sd[f"{pre}.{n}.{i}.beta"] = t(0.1 * rng.standard_normal(H))
+
+    def affine(name):
+        tr = 0.2 * rng.standard_normal((2, 1))
+        tr[0, 0] -= log_duration
+        sd[f"{name}.translation"] = t(tr)
+        sd[f"{name}.log_scale"] = t(0.1 * rng.standard_normal((2, 1)))
+
+    def conv_flow(name):
+        conv(f"{name}.pre", H, 1, 1)
+        dds(f"{name}.convs")
+        conv(f"{name}.proj", 3 * nb - 1, H, 1, scale=np.sqrt(0.5), bias_std=0.1)
+
+    conv("pre", H, in_channels, 1)
+    dds("convs")
+    conv("proj", H, H, 1)
+    affine("flows.0")
+    for f in range(num_flows):
+        conv_flow(f"flows.{f + 1}")
+    conv("post_pre", H, 1, 1)
+    dds("post_convs")
+    conv("post_proj", H, H, 1)
+    affine("post_flows.0")
+    for f in range(num_flows):
+        conv_flow(f"post_flows.{f + 1}")
+    if cond_channels:
+        conv("cond", H, cond_channels, 1)
+    return sd
 
 
 def tokens(batch: int, length: int, num_chars: int, seed: int = 0) -> torch.Tensor:
