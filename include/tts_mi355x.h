@@ -424,6 +424,91 @@ int tts_vits_posterior_forward_profiled(void* handle, const float* d_x, const fl
                                         int max_records, int* n_records);
 
 /* ------------------------------------------------------------------------------------ */
+/* VITS text side of Vits.inference (TTS/tts/models/vits.py:1121-1155), since ABI 114       */
+/* ------------------------------------------------------------------------------------ */
+
+/* Mirrors TextEncoder.__init__ (TTS/tts/layers/vits/networks.py:29-81; VITS builds it at
+ * vits.py:653-663 with out = hidden = hidden_channels).  The transformer is the Glow encoder's
+ * RelativePositionTransformer with layer_norm_type "2" and rel_attn_window_size 4. */
+typedef struct TtsVitsTextEncoderCfg {
+  int n_vocab;             /* num_chars */
+  int out_channels;        /* 192 */
+  int hidden_channels;     /* 192 */
+  int hidden_channels_ffn; /* 768 */
+  int num_heads;           /* 2 */
+  int num_layers;          /* 6 */
+  int kernel_size;         /* 3 (FFN) */
+  int language_emb_dim;    /* must be 0 (multilingual concat not implemented) */
+  int math_mode;           /* TTS_MATH_FP32, _X6 or TTS_MATH_BF16 */
+} TtsVitsTextEncoderCfg;
+
+/* Host weight order: emb.weight [n_vocab][H]; per layer l: encoder.attn_layers.l.conv_q/k/v/o
+ * (weight [H][H][1], bias [H]), emb_rel_k [1][9][dk], emb_rel_v [1][9][dk], encoder.norm_layers_1.l
+ * gamma [H], beta [H], encoder.ffn_layers.l.conv_1 (weight [ffn][H][k], bias), conv_2 (weight
+ * [H][ffn][k], bias), encoder.norm_layers_2.l gamma, beta; proj.weight [2 out][H][1], proj.bias [2 out]. */
+int tts_vits_text_encoder_num_weights(const TtsVitsTextEncoderCfg* cfg);
+int64_t tts_vits_text_encoder_weight_numel(const TtsVitsTextEncoderCfg* cfg, int index);
+int tts_vits_text_encoder_create(const TtsVitsTextEncoderCfg* cfg, const float* const* host_weights, int device,
+                                 void** handle);
+int tts_vits_text_encoder_destroy(void* handle);
+/* (x, m, logs, x_mask) = TextEncoder.forward(tokens, lengths) (networks.py:83-100): tokens [B][T] int64,
+ * lengths [B] int64; x [B][H][T], m and logs [B][out][T], x_mask [B][1][T].  T <= 3072. */
+int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
+                                  float* d_x, float* d_m, float* d_logs, float* d_x_mask, void* hip_stream);
+int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
+                                           int T, float* d_x, float* d_m, float* d_logs, float* d_x_mask,
+                                           void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                           int* n_records);
+
+/* Mirrors StochasticDurationPredictor.__init__ (TTS/tts/layers/vits/stochastic_duration_predictor.py:
+ * 185-227; VITS: in = hidden_channels, hidden 192, kernel 3, 4 flows, cond = embedded_speaker_dim when
+ * condition_dp_on_speaker, vits.py:684-692).  ConvFlows use 10 bins, tail bound 5 (:96-104). */
+typedef struct TtsVitsSdpCfg {
+  int in_channels;      /* 192 */
+  int hidden_channels;  /* 192 */
+  int kernel_size;      /* 3 */
+  int num_flows;        /* 4 */
+  int cond_channels;    /* 0 = no cond layer */
+  int language_emb_dim; /* must be 0 */
+  int math_mode;        /* TTS_MATH_FP32, _X6 or TTS_MATH_BF16 (its 1x1 convs) */
+} TtsVitsSdpCfg;
+
+/* Host weight order (the inference-side tensors in state_dict order; post_* are training-only):
+ *   pre.weight [H][in][1], pre.bias [H]
+ *   DDS(convs): convs_sep.i.weight [H][1][k], bias [H] (i < 3); convs_1x1.i.weight [H][H][1], bias [H];
+ *               norms_1.i.gamma [H], beta [H]; norms_2.i.gamma [H], beta [H]
+ *   proj.weight [H][H][1], proj.bias [H]
+ *   flows.0.translation [2][1], flows.0.log_scale [2][1]
+ *   for f = 1 .. num_flows: flows.f.pre.weight [H][1][1], bias [H]; DDS(flows.f.convs);
+ *                           flows.f.proj.weight [29][H][1], bias [29]
+ *   if cond_channels: cond.weight [H][cond][1], cond.bias [H] */
+int tts_vits_sdp_num_weights(const TtsVitsSdpCfg* cfg);
+int64_t tts_vits_sdp_weight_numel(const TtsVitsSdpCfg* cfg, int index);
+int tts_vits_sdp_create(const TtsVitsSdpCfg* cfg, const float* const* host_weights, int device, void** handle);
+int tts_vits_sdp_destroy(void* handle);
+/* logw [B][1][T] = StochasticDurationPredictor.forward(x, x_mask, g=g, reverse=True, noise_scale)
+ * (:242-282): x [B][in][T], x_mask [B][1][T], g [B][cond_channels] or NULL, noise [B][2][T] the
+ * standard normal draw of :277 (torch.randn(B, 2, T); NULL = zeros). */
+int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g, const float* d_noise,
+                         float noise_scale, int B, int T, float* d_logw, void* hip_stream);
+int tts_vits_sdp_reverse_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                                  const float* d_noise, float noise_scale, int B, int T, float* d_logw,
+                                  void* hip_stream, TtsLaunchRecord* records, int max_records, int* n_records);
+
+/* vits.py:1145-1148: w_ceil [B][1][T_x] = ceil(exp(logw) * x_mask * length_scale); y_lengths [B]
+ * (int64) = max(sum(w_ceil), 1).  The caller reads y_lengths back for T_y = max(y_lengths). */
+int tts_vits_durations(const float* d_logw, const float* d_x_mask, int B, int T_x, float length_scale,
+                       float* d_w_ceil, int64_t* d_y_lengths, void* hip_stream);
+/* vits.py:1147-1154: y_mask [B][1][T_y]; attn = generate_path(w_ceil, x_mask * y_mask) [B][T_x][T_y]
+ * (may be NULL); m_p' = attn^T m_p, logs_p' = attn^T logs_p ([B][C][T_y], may be NULL);
+ * z_p = m_p' + noise * exp(logs_p') * noise_scale (not masked; noise [B][C][T_y] NULL = zeros).
+ * T_y >= max(y_lengths), T_x <= 16384. */
+int tts_vits_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t* d_y_lengths, const float* d_m_p,
+                    const float* d_logs_p, const float* d_noise, float noise_scale, int B, int C, int T_x, int T_y,
+                    float* d_z_p, float* d_y_mask, float* d_m_p_out, float* d_logs_p_out, float* d_attn,
+                    void* hip_stream);
+
+/* ------------------------------------------------------------------------------------ */
 /* Single-op entry points (test / tuning surface).  These pack the host weights into a     */
 /* temporary device buffer on every call and synchronise; they are not the hot path.        */
 /* ------------------------------------------------------------------------------------ */

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == N.ABI_VERSION == 113
+    assert N.lib().tts_abi_version() == N.ABI_VERSION == 114
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -458,3 +458,33 @@ def test_xtts_generator_inventory_and_validation():
         assert N.lib().tts_hifigan_weight_numel(ctypes.byref(g._cfg), i) == w.size
     with pytest.raises(N.NativeError):
         HifiganGenerator(**dict(cfg, cond_channels=0), cond_in_each_up_layer=True)
+
+
+def test_vits_text_weight_inventories_match_modules():
+    """TextEncoder / StochasticDurationPredictor: the tensors the drop-ins hand over (reference
+    state_dict order) match the C-ABI inventory element by element; unsupported configurations are
+    rejected with the documented codes (no GPU needed)."""
+    from tts_amd.config import VITS_SDP, VITS_TEXT_ENCODER
+    from tts_amd.tts import StochasticDurationPredictor, TextEncoder
+
+    te = TextEncoder(64, 192, 192, 768, 2, 6, 3, 0.1)
+    te.load_state_dict(synthetic.vits_text_encoder_state_dict(num_chars=64, **VITS_TEXT_ENCODER))
+    ws = te._weight_list()
+    assert len(ws) == N.lib().tts_vits_text_encoder_num_weights(ctypes.byref(te._cfg))
+    for i, w in enumerate(ws):
+        assert w.size == N.lib().tts_vits_text_encoder_weight_numel(ctypes.byref(te._cfg), i), i
+    for gin in (0, 16):
+        sdp = StochasticDurationPredictor(192, 192, 3, 0.5, 4, cond_channels=gin)
+        sdp.load_state_dict(synthetic.vits_sdp_state_dict(**VITS_SDP, cond_channels=gin))
+        ws = sdp._weight_list()
+        assert len(ws) == N.lib().tts_vits_sdp_num_weights(ctypes.byref(sdp._cfg))
+        for i, w in enumerate(ws):
+            assert w.size == N.lib().tts_vits_sdp_weight_numel(ctypes.byref(sdp._cfg), i), i
+    c = N.TtsVitsSdpCfg(192, 192, 3, 4, 0, 0, N.MATH_MODES["f16x3"])
+    assert N.lib().tts_vits_sdp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c = N.TtsVitsSdpCfg(192, 192, 3, 4, 0, 8, N.MATH_MODES["fp32"])  # language embeddings
+    assert N.lib().tts_vits_sdp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    t = N.TtsVitsTextEncoderCfg(64, 192, 192, 768, 3, 6, 3, 0, 0)  # 192 % 3 == 0 but dk = 64: fine
+    assert N.lib().tts_vits_text_encoder_num_weights(ctypes.byref(t)) > 0
+    t = N.TtsVitsTextEncoderCfg(64, 192, 192, 768, 5, 6, 3, 0, 0)  # channels not divisible by heads
+    assert N.lib().tts_vits_text_encoder_num_weights(ctypes.byref(t)) == -N.TTS_ERR_INVALID

@@ -518,3 +518,25 @@ def test_long_utterance_beyond_plane_cap(cuda_device, mode):
         ref = hifigan_ref.hifigan_forward(sd, _padded_slice(mel, pad, lo, hi), pad=0, dtype=torch.float64, **V1)
         ref = ref[:, :, 256 * (a - lo):256 * (b - lo)]
         assert_close_fp32(y[:, :, 256 * a:256 * b], ref, f"long utterance frames [{a},{b}) ({mode})", **tol(mode))
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "fp32x6", "bf16"])
+def test_conv_post_fusion_bitwise(cuda_device, monkeypatch, mode):
+    """conv_post inside the last MRF pair launch (ResPairArgs::post_w: tiles overlapping by conv_post's
+    3-sample halo, the final z kept in LDS) against the separate conv_post launch
+    (TTS_MI355X_POST_FUSION=0): the same fp32 operations in the same order, so bitwise equal, at
+    lengths that end inside, exactly on and just past a tile (240-sample stride at k11 / c32)."""
+    sd = synthetic.hifigan_state_dict(seed=51, weight_norm=False)
+    for B, T in [(2, 37), (1, 15), (3, 61)]:
+        mel = synthetic.mel(B, T, seed=T).to(cuda_device)
+        outs = {}
+        for fused in ("1", "0"):
+            monkeypatch.setenv("TTS_MI355X_POST_FUSION", fused)
+            g = HifiganGenerator(**V1, math_mode=mode)
+            g.remove_weight_norm()
+            g.load_state_dict(sd)
+            g = g.to(cuda_device)
+            outs[fused] = g.inference(mel)
+            names = [r["name"] for r in g.profile(mel)[1]]
+            assert ("conv_post" in names) == (fused == "0"), names[-3:]
+        assert torch.equal(outs["1"], outs["0"]), (B, T, (outs["1"] - outs["0"]).abs().max().item())

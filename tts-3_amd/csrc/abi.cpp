@@ -69,7 +69,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 113; }
+int tts_abi_version(void) { return 114; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -240,6 +240,158 @@ int tts_glow_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t*
     a.o_log_scale = d_o_log_scale; a.noise = d_noise; a.noise_scale = noise_scale;
     a.C = C; a.T_x = T_x; a.T_y = T_y;
     a.z = d_z; a.y_mask = d_y_mask; a.y_mean = d_y_mean; a.y_log_scale = d_y_log_scale; a.attn = d_attn;
+    tts::launch_expand(a, B, static_cast<hipStream_t>(hip_stream));
+    TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+// ----------------------------------------------------------------------------- VITS text side
+int tts_vits_text_encoder_num_weights(const TtsVitsTextEncoderCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_text_encoder_validate(*cfg);
+    n = (int)tts::vits_text_encoder_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_vits_text_encoder_weight_numel(const TtsVitsTextEncoderCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_text_encoder_validate(*cfg);
+    auto s = tts::vits_text_encoder_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_vits_text_encoder_create(const TtsVitsTextEncoderCfg* cfg, const float* const* host_weights, int device,
+                                 void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::VitsTextEncoder(*cfg, host_weights, device);
+  });
+}
+
+int tts_vits_text_encoder_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::VitsTextEncoder*>(handle); });
+}
+
+int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
+                                  float* d_x, float* d_m, float* d_logs, float* d_x_mask, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::VitsTextEncoder*>(handle)->forward(d_tokens, d_lengths, B, T, d_x, d_m, d_logs, d_x_mask,
+                                                        static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
+                                           int T, float* d_x, float* d_m, float* d_logs, float* d_x_mask,
+                                           void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                           int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::VitsTextEncoder*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->forward(d_tokens, d_lengths, B, T, d_x, d_m, d_logs, d_x_mask, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+int tts_vits_sdp_num_weights(const TtsVitsSdpCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_sdp_validate(*cfg);
+    n = (int)tts::vits_sdp_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_vits_sdp_weight_numel(const TtsVitsSdpCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_sdp_validate(*cfg);
+    auto s = tts::vits_sdp_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_vits_sdp_create(const TtsVitsSdpCfg* cfg, const float* const* host_weights, int device, void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::VitsSdp(*cfg, host_weights, device);
+  });
+}
+
+int tts_vits_sdp_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::VitsSdp*>(handle); });
+}
+
+int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g, const float* d_noise,
+                         float noise_scale, int B, int T, float* d_logw, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::VitsSdp*>(handle)->reverse(d_x, d_x_mask, d_g, d_noise, noise_scale, B, T, d_logw,
+                                                static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_sdp_reverse_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                                  const float* d_noise, float noise_scale, int B, int T, float* d_logw,
+                                  void* hip_stream, TtsLaunchRecord* records, int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::VitsSdp*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->reverse(d_x, d_x_mask, d_g, d_noise, noise_scale, B, T, d_logw, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+int tts_vits_durations(const float* d_logw, const float* d_x_mask, int B, int T_x, float length_scale,
+                       float* d_w_ceil, int64_t* d_y_lengths, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_logw && d_x_mask && d_w_ceil && d_y_lengths, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && T_x >= 1, 1, "batch and token count must be >= 1");
+    tts::launch_durations(d_logw, d_x_mask, d_w_ceil, d_y_lengths, nullptr, B, T_x, length_scale,
+                          static_cast<hipStream_t>(hip_stream), 1);
+    TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+int tts_vits_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t* d_y_lengths, const float* d_m_p,
+                    const float* d_logs_p, const float* d_noise, float noise_scale, int B, int C, int T_x, int T_y,
+                    float* d_z_p, float* d_y_mask, float* d_m_p_out, float* d_logs_p_out, float* d_attn,
+                    void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_w_ceil && d_x_mask && d_y_lengths && d_m_p && d_logs_p && d_z_p && d_y_mask, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && C >= 1 && T_x >= 1 && T_y >= 1, 1, "bad expand shape");
+    tts::ExpandArgs a{};
+    a.w_ceil = d_w_ceil; a.x_mask = d_x_mask; a.y_len = d_y_lengths; a.o_mean = d_m_p;
+    a.o_log_scale = d_logs_p; a.noise = d_noise; a.noise_scale = noise_scale;
+    a.C = C; a.T_x = T_x; a.T_y = T_y;
+    a.z = d_z_p; a.y_mask = d_y_mask; a.y_mean = d_m_p_out; a.y_log_scale = d_logs_p_out; a.attn = d_attn;
+    a.vits = 1;
     tts::launch_expand(a, B, static_cast<hipStream_t>(hip_stream));
     TTS_HIP_CHECK(hipGetLastError());
   });

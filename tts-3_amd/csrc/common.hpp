@@ -94,6 +94,14 @@ inline int gate_row_order(int rho, int H) {
 struct ResPairArgs {
   Conv1dArgs c1;
   Conv1dArgs c2;
+  // post_w != nullptr (the generator's last MRF writer, c2.zmode 3): conv_post fused into the
+  // epilogue (hifigan_generator.py:262-264): wav[b][t] = tanh(post_bias + sum_c,k post_w[c][k] *
+  // lrelu(z[c][t - 3 + k], post_slope)) with z the final MRF sum, which is not stored.  Tiles then
+  // overlap by 6 columns (3 of conv_post's halo on each side).
+  const float* post_w;  // [C][7]
+  float post_bias;
+  float post_slope;
+  float* wav;           // [B][1][T]
 };
 bool resblock_pair_supported(int mode, int C, int K, int dil);
 bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster

@@ -26,7 +26,7 @@ constexpr double kBnEps = 1e-5;  // nn.BatchNorm1d default
 int odd_k(int k) { return k % 2 ? k : k + 1; }
 }  // namespace
 
-std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp) {
   std::vector<int64_t> n;
   const int64_t H = c.hidden_channels, F = c.hidden_channels_ffn, K = c.kernel_size, D = c.hidden_channels_dp;
   const int et = c.encoder_type;
@@ -71,6 +71,7 @@ std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c) {
   }
   n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels);  // proj_m
   if (!c.mean_only) { n.push_back((int64_t)c.out_channels * H); n.push_back(c.out_channels); }  // proj_s
+  if (!with_dp) return n;
   // dp conv_1 reads cat(x, g) when speaker-conditioned (encoder.py:166-168: H + c_in channels)
   n.push_back(D * (H + c.c_in_channels) * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_1, norm_1
   n.push_back(D * D * 3); n.push_back(D); n.push_back(D); n.push_back(D);  // dp conv_2, norm_2
@@ -119,11 +120,11 @@ void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
               "Glow encoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
-GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, int device)
-    : cfg_(cfg), device_(device) {
+GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, int device, bool with_dp)
+    : cfg_(cfg), device_(device), with_dp_(with_dp) {
   glow_encoder_validate(cfg_);
   DeviceGuard g(device_);
-  const auto shapes = glow_encoder_weight_shapes(cfg_);
+  const auto shapes = glow_encoder_weight_shapes(cfg_, with_dp_);
   for (size_t i = 0; i < shapes.size(); ++i)
     TTS_REQUIRE(hw[i] != nullptr, 1, "weight pointer " + std::to_string(i) + " is NULL");
   const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, K = cfg_.kernel_size;
@@ -279,12 +280,14 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
     put_conv(proj_s_, {{hw[wi], hw[wi + 1]}}, cfg_.out_channels, H, 1);
     wi += 2;
   }
-  put_conv(dp1_, {{hw[wi], hw[wi + 1]}}, D, H + cfg_.c_in_channels, 3);
-  put_norm(dpn1_, hw[wi + 2], hw[wi + 3], D);
-  put_conv(dp2_, {{hw[wi + 4], hw[wi + 5]}}, D, D, 3);
-  put_norm(dpn2_, hw[wi + 6], hw[wi + 7], D);
-  put_conv(dp_proj_, {{hw[wi + 8], hw[wi + 9]}}, 1, D, 1);
-  wi += 10;
+  if (with_dp_) {
+    put_conv(dp1_, {{hw[wi], hw[wi + 1]}}, D, H + cfg_.c_in_channels, 3);
+    put_norm(dpn1_, hw[wi + 2], hw[wi + 3], D);
+    put_conv(dp2_, {{hw[wi + 4], hw[wi + 5]}}, D, D, 3);
+    put_norm(dpn2_, hw[wi + 6], hw[wi + 7], D);
+    put_conv(dp_proj_, {{hw[wi + 8], hw[wi + 9]}}, 1, D, 1);
+    wi += 10;
+  }
   TTS_REQUIRE(wi == shapes.size(), 2, "internal: Glow encoder weight count mismatch");
 
   if (hipMalloc(&arena_, host.size() * sizeof(float)) != hipSuccess) throw Error(4, "hipMalloc(weights) failed");
@@ -311,8 +314,8 @@ void GlowEncoder::reserve(int B, int T) {
 }
 
 void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m,
-                          float* x_logs, float* logw, float* x_mask, hipStream_t s, Profiler* prof) {
-  TTS_REQUIRE(tok && len && x_m && logw && x_mask, 1, "NULL input/output pointer");
+                          float* x_logs, float* logw, float* x_mask, hipStream_t s, Profiler* prof, float* x_out) {
+  TTS_REQUIRE(tok && len && x_m && x_mask && (logw || !with_dp_), 1, "NULL input/output pointer");
   TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1 && T >= 1, 1, "batch and token count must be >= 1");
   // the attention kernel keeps whole score rows in LDS; the convolutional encoder types have no such bound
@@ -438,6 +441,7 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
     conv("enc_ffn2", L.ffn2, Wd, x, other, mask, 1.f, false);            // x + conv_2(h*mask)*mask
     norm("enc_layernorm", L.n2, x, nullptr, x, H, false, eps_tf);          // norm_layers_2, * mask
   }
+  if (x_out) TTS_HIP_CHECK(hipMemcpyAsync(x_out, x, plane * H * sizeof(float), hipMemcpyDeviceToDevice, s));
   // heads (encoder.py:171-178)
   conv("enc_proj_m", proj_m_, x, x_m, nullptr, mask, 1.f, false);
   if (!cfg_.mean_only) {
@@ -446,6 +450,7 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
   } else if (x_logs) {
     TTS_HIP_CHECK(hipMemsetAsync(x_logs, 0, plane * cfg_.out_channels * sizeof(float), s));
   }
+  if (!with_dp_) return;
   // duration predictor (duration_predictor.py:63-73) on x (detached: same values), or on
   // cat(x, g.expand(T)) for a speaker-conditioned model (encoder.py:166-168; the predictor masks
   // its whole input, :66, and x is already masked)

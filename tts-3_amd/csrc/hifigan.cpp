@@ -105,6 +105,8 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   // TTS_MI355X_NO_PAIR_FUSION=1 keeps every resblock conv a separate launch (the tests' reference arm)
   const char* nf = std::getenv("TTS_MI355X_NO_PAIR_FUSION");
   const bool pair_fusion = !(nf && nf[0] == '1');
+  const char* pf = std::getenv("TTS_MI355X_POST_FUSION");
+  post_fusion_ = !(pf && pf[0] == '0');
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
@@ -480,6 +482,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
 
   const int L = T + 2 * pad;
   const int C0 = cfg_.upsample_initial_channel;
+  bool post_done = false;  // conv_post ran inside the last MRF launch (ResPairArgs::post_w)
   if (cvec) {
     run(prof, s, "cond_layer", 2.0 * B * C0 * cfg_.cond_channels, 4.0 * (B * cfg_.cond_channels + C0 * cfg_.cond_channels + B * C0),
         [&] { launch_cond_vec(gvec, cond_wd_, cond_bd_, cvec, B, cfg_.cond_channels, C0, s); });
@@ -583,10 +586,24 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
           c2.n_chunks = L2.n_chunks; c2.in_slope = 1.f; c2.out_slope = 1.f; c2.zmode = last ? zlast : 0;
           c2.zdiv = (float)cfg_.num_kernels; c2.w_exp = L2.w_exp;
           c2.amax_out = last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1);
-          const double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
-          const double bytes = 4.0 * ((double)B * L1.Cout * len * (last ? (zlast >= 2 ? 4 : 3) : 3) +
-                                      2.0 * L1.Cout * L1.Cin * L1.K);
-          const std::string nm = "mrf_pair_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
+          // the generator's last MRF writer: conv_post runs in its epilogue (the final z never
+          // reaches HBM); TTS_MI355X_POST_FUSION=0 keeps the separate conv_post launch
+          const bool post = last && zlast == 3 && i == cfg_.num_upsamples - 1 && post_fusion_ &&
+                            cfg_.out_channels == 1;
+          if (post) {
+            pa.post_w = post_wd_; pa.post_bias = post_bias_; pa.post_slope = 0.01f; pa.wav = wav;
+            c2.amax_out = nullptr;  // nothing reads the final z's statistics
+            post_done = true;
+          }
+          double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
+          double bytes = 4.0 * ((double)B * L1.Cout * len * (last ? (zlast >= 2 ? 4 : 3) : 3) +
+                                2.0 * L1.Cout * L1.Cin * L1.K);
+          if (post) {
+            flops += 2.0 * B * len * (double)L1.Cout * 7;
+            bytes += 4.0 * ((double)B * len - (double)B * L1.Cout * len);  // + wav, - the z store
+          }
+          const std::string nm = std::string(post ? "mrf_pair_post_k" : "mrf_pair_k") + std::to_string(L1.K) +
+                                 "_c" + std::to_string(L1.Cout);
           run(prof, s, nm.c_str(), flops, bytes, [&] { launch_resblock_pair(L1.mode, pa, B, L1.K, L1.Cout, s); });
         }
       } else if (cfg_.resblock_type == 1) {
@@ -614,6 +631,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
     cur = bufZ;
   }
   // leaky_relu (default slope 0.01!) -> conv_post -> tanh (:262-264)
+  if (post_done) return;
   PostArgs pa{};
   pa.z = bufZ; pa.w = post_wd_; pa.bias = post_bias_; pa.y = wav;
   pa.Cin = C0 >> cfg_.num_upsamples; pa.T = len; pa.in_slope = 0.01f;

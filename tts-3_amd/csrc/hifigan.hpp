@@ -118,6 +118,7 @@ class Hifigan {
   TtsHifiganCfg cfg_;
   int device_;
   int hop_ = 1;
+  bool post_fusion_ = true;  // conv_post inside the last MRF launch (TTS_MI355X_POST_FUSION=0: off)
   ConvLayer pre_;
   std::vector<ConvTLayer> ups_;
   std::vector<ResBlock> res_;

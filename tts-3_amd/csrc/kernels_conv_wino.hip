@@ -8,9 +8,16 @@
 
 namespace tts {
 
+// f16x3 (fp32-faithful), and bf16 (configs 3 / 5: one bf16 product per transformed point, the
+// transforms in fp32; rel-RMS against fp64 in tests/test_configs_gpu.py's bf16 gate).  bf16 is the
+// default there unless TTS_MI355X_WINO_BF16=0.
 bool wino_supported(int mode, int Cout, int Cin, int K, int dil) {
-  return mode == MATH_FP32_F16X3 && Cout % 128 == 0 && Cin % 16 == 0 && (K == 3 || K == 7 || K == 11) &&
-         (dil == 1 || dil == 3 || dil == 5);
+  bool m = mode == MATH_FP32_F16X3;
+  if (mode == MATH_BF16) {
+    const char* e = std::getenv("TTS_MI355X_WINO_BF16");
+    m = !(e && e[0] == '0');
+  }
+  return m && Cout % 128 == 0 && Cin % 16 == 0 && (K == 3 || K == 7 || K == 11) && (dil == 1 || dil == 3 || dil == 5);
 }
 
 // TTS_MI355X_WINO=0 keeps the direct split kernel for every conv (A/B runs, accuracy comparisons)
@@ -27,8 +34,13 @@ void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
               "conv1d: a batch item's channel plane exceeds 2 GiB");
   // the 8-wave form needs 16-byte aligned input rows (every HiFiGAN MRF conv at >= 128 channels:
   // T = 8 * (T_mel + 2 pad) and more); other lengths take the 4-wave form
-  if (a.Tin % 4 == 0) wino8_detail::launch_s<SchemeH3>(a, B, K, s);
-  else wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
+  if (mode == MATH_BF16) {
+    if (a.Tin % 4 == 0) wino8_detail::launch_s<SchemeB1>(a, B, K, s);
+    else wino_detail::launch_wino_s<SchemeB1>(a, B, K, s);
+  } else {
+    if (a.Tin % 4 == 0) wino8_detail::launch_s<SchemeH3>(a, B, K, s);
+    else wino_detail::launch_wino_s<SchemeH3>(a, B, K, s);
+  }
   TTS_HIP_CHECK(hipGetLastError());
 }
 

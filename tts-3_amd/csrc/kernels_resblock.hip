@@ -32,7 +32,10 @@ namespace tts {
 #define RES_STAGE_8R 1  // x staging lane map of the pair / whole-block kernels (0: 4 rows x 4 quads)
 #endif
 
-template <class S, int K, int C, int PD, int GEO, bool ALLX = false>
+constexpr int kPostK = 7;     // conv_post kernel (hifigan_generator.py:229-230)
+constexpr int kPostHalo = 3;  // its zero-padding halo per side
+
+template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
   static constexpr int RP_W = GEO == 0 ? 256 : 192;
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
@@ -50,17 +53,22 @@ struct PairCfg {
   // ALLX: every 16-channel group of the input window is staged at once (one HBM latency for the
   // whole of phase 1, no per-chunk barriers); otherwise double-buffered per group
   static constexpr int XBUFS = ALLX ? NC : 2;
-  static constexpr int LDSB = (XBUFS * XSZB > TSZB ? XBUFS * XSZB : TSZB);
+  static constexpr int LDSB0 = (XBUFS * XSZB > TSZB ? XBUFS * XSZB : TSZB);
+  // POST: the final z tile (fp32 [C][RP_BN]) for the fused conv_post, after phase 2
+  static constexpr int ZTB = POST ? C * RP_BN * 4 : 0;
+  static constexpr int LDSB = LDSB0 > ZTB ? LDSB0 : ZTB;
+  // POST: output tiles overlap by conv_post's halo on both sides
+  static constexpr int STRIDE = POST ? RP_BN - 2 * kPostHalo : RP_BN;
   static constexpr int UPT = (XROWS * 4 + 255) / 256;
   static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
 // C = 32 (16-bit-pair schemes): ask for 3 waves per SIMD (<= 168 VGPRs + AGPRs): the LDS already
 // allows three workgroups per CU, the unconstrained allocation (173) allowed two
-template <class S, int K, int C, int PD, int GEO, bool ALLX>
+template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 && S::ROWB <= 80 ? 3 : 1)))
 void resblock_pair_kernel(ResPairArgs pa) {
-  using P = PairCfg<S, K, C, PD, GEO, ALLX>;
+  using P = PairCfg<S, K, C, PD, GEO, ALLX, POST>;
   constexpr int RP_W = P::RP_W, RP_BN = P::RP_BN;
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
@@ -80,13 +88,71 @@ void resblock_pair_kernel(ResPairArgs pa) {
   const int wm = __builtin_amdgcn_readfirstlane(wave / P::WN);
   const int wn = wave % P::WN;
   const int mrow0 = wm * TM * 32;  // first output channel of this wave
-  const int t0 = blockIdx.x * RP_BN;
+  const int t0 = (int)blockIdx.x * P::STRIDE - (POST ? kPostHalo : 0);
   const int b = blockIdx.z;
   const int d = a1.dil;
   const int T = a1.Tout;
   const int XW = RP_W + (K - 1) * d;
   const int tx0 = t0 - P::LEAD;  // time of convs1 column 0
   const unsigned avoff = (unsigned)lane * 16u;
+
+  // POST: the final MRF sum of this tile, v = (z + convs2(xt) + bias + x) / zdiv exactly as
+  // conv_epilogue_impl<RES, ZM = 3> forms it, into LDS (zero outside [0, T): conv_post's zero
+  // padding); then conv_post on the inner columns [3, RP_BN - 3), one column per thread, with
+  // conv_post4_kernel's FMA order (bias, then channel by channel, tap by tap), and tanh
+  auto post_epilogue = [&](const ResPairArgs& q, const f32x16 (&ac)[TM][TN], int bb, int tt0, int row0w, int wnn,
+                           int ln) {
+    const Conv1dArgs a2 = q.c2;
+    const int hf = ln >> 5, lo = ln & 31;
+    const size_t item = (size_t)bb * C * T;
+    const unsigned plane = (unsigned)C * (unsigned)T * 4u;
+    const rsrc_t rres = make_rsrc(a2.res + item, plane);
+    const rsrc_t rz = make_rsrc(a2.z + item, plane);
+    const unsigned rowb = (unsigned)T * 4u;
+    float* zt = reinterpret_cast<float*>(smem);
+    __syncthreads();  // every wave is past its last phase-2 read of xt
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int col = wnn * TN * 32 + n * 32 + lo;
+        const int t = tt0 + col;
+        const bool tok = t >= 0 && t < T && col < RP_BN;
+        const int rw0 = row0w + m * 32 + 4 * hf;
+        const unsigned voff = tok ? ((unsigned)rw0 * (unsigned)T + (unsigned)t) * 4u : OOB_OFF;
+        float rv[16], zv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const unsigned vo = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
+          rv[r] = bload(rres, vo, 0u);
+          zv[r] = bload(rz, vo, 0u);
+        }
+        if (col < RP_BN) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = rw0 + (r & 3) + 8 * (r >> 2);
+            float v = (ac[m][n][r] + bsm[C + row]) * 1.f;
+            v = lrelu2(v, a2.out_slope);
+            v = (v + rv[r]) * 1.f;
+            v = (zv[r] + v) / a2.zdiv;
+            zt[row * RP_BN + col] = tok ? v : 0.f;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int col = kPostHalo + tid;
+    const int t = tt0 + col;
+    if (col < RP_BN - kPostHalo && t >= 0 && t < T) {
+      float o = q.post_bias;
+      for (int ci = 0; ci < C; ++ci) {
+        const float* zr = zt + ci * RP_BN + col - kPostHalo;
+#pragma unroll
+        for (int k = 0; k < kPostK; ++k) o = fmaf(q.post_w[ci * kPostK + k], lrelu(zr[k], q.post_slope), o);
+      }
+      q.wav[(size_t)bb * T + t] = tanhf(o);
+    }
+  };
 
   // ------------------------------------------------------------------ phase 1: convs1
   const int ex = H3 ? amax_exp(a1.amax_in, b) : 0;
@@ -321,18 +387,27 @@ void resblock_pair_kernel(ResPairArgs pa) {
 #pragma unroll
         for (int n = 0; n < TN; ++n) acc[m][n] *= sc2;
     }
-    // C = 64: the software-pipelined epilogue (one memory latency per tile; registers allow it)
-    conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
+    if constexpr (POST) {
+      post_epilogue(pa, acc, b, t0, mrow0, wn, lane);
+    } else {
+      conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
+    }
   }
 }
 
 namespace {
 template <class S, int K, int C, int GEO>
 void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
+  constexpr bool AX = C == 64;  // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32
+  if (a.post_w) {
+    using P = PairCfg<S, K, C, 2, GEO, AX, true>;
+    static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
+    dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
+    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, true>), grid, dim3(256), 0, s, a);
+    return;
+  }
   dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
-  // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32 (scripts/ab_pair_allx.sh)
-  if (C == 64) hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, false>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX>), grid, dim3(256), 0, s, a);
 }
 
 template <class S, int K>
@@ -373,6 +448,8 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
   TTS_REQUIRE(a.c1.cvec == nullptr && a.c2.cvec == nullptr && a.c1.bias && a.c2.bias, 1,
               "resblock pair: biases required, no cond vector (both are staged in LDS)");
   TTS_REQUIRE((int64_t)C * a.c1.Tout * 4 < (int64_t(1) << 31), 3, "resblock pair: plane exceeds 2 GiB");
+  TTS_REQUIRE(!a.post_w || (a.c2.zmode == 3 && a.c2.res && a.c2.z && a.wav && !a.c2.mask), 1,
+              "resblock pair: the fused conv_post needs the final MRF sum (zmode 3) with a residual");
   if (mode == MATH_FP32_F16X3) launch_pair_s<SchemeH3>(a, B, K, C, s);
   else if (mode == MATH_BF16) launch_pair_s<SchemeB1>(a, B, K, C, s);
   else launch_pair_s<SchemeX6>(a, B, K, C, s);

@@ -433,16 +433,19 @@ void launch_attention(const float* qkv, const float* mask, const float* ek, cons
 // (the sum over frames of token i's alignment row is w_ceil[i] for every unmasked token, since
 // y_len >= the cumulative duration of every token).  Sums of integers < 2^24 are exact in fp32.
 // ---------------------------------------------------------------------------------------
+// vits = 1 (vits.py:1145-1148): w = exp(logw) * x_mask * length_scale, w_ceil = ceil(w) (a token may
+// get 0 frames), no o_attn_dur.
 __global__ void __launch_bounds__(256) durations_kernel(const float* __restrict__ logw, const float* __restrict__ xm,
                                                         float* __restrict__ w_ceil, int64_t* __restrict__ y_len,
-                                                        float* __restrict__ dur, int T, float length_scale) {
+                                                        float* __restrict__ dur, int T, float length_scale, int vits) {
   __shared__ float part[4];
   const int b = blockIdx.x;
   float s = 0.f;
   for (int t = threadIdx.x; t < T; t += 256) {
     const float m = xm[(size_t)b * T + t];
-    const float w = (expf(logw[(size_t)b * T + t]) - 1.f) * m * length_scale;
-    const float wc = fmaxf(ceilf(w), 1.f);
+    const float e = expf(logw[(size_t)b * T + t]);
+    const float w = (vits ? e : e - 1.f) * m * length_scale;
+    const float wc = vits ? ceilf(w) : fmaxf(ceilf(w), 1.f);
     w_ceil[(size_t)b * T + t] = wc;
     if (dur) dur[(size_t)b * T + t] = logf(1.f + wc * m) * m;
     s += wc;
@@ -458,13 +461,14 @@ __global__ void __launch_bounds__(256) durations_kernel(const float* __restrict_
 }
 
 void launch_durations(const float* logw, const float* xm, float* w_ceil, int64_t* y_len, float* dur, int B, int T,
-                      float length_scale, hipStream_t s) {
-  hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, s, logw, xm, w_ceil, y_len, dur, T, length_scale);
+                      float length_scale, hipStream_t s, int vits) {
+  hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, s, logw, xm, w_ceil, y_len, dur, T, length_scale, vits);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------------
-// Alignment expansion (glow_tts.py:353-361, helpers.py:154-169, compute_outputs :138-148).
+// Alignment expansion (glow_tts.py:353-361, helpers.py:154-169, compute_outputs :138-148; VITS:
+// vits.py:1147-1154).
 // Token i covers frames [cum[i-1], cum[i]) with cum the inclusive cumsum of w_ceil; attn[i][j]
 // = that indicator * x_mask[i] * y_mask[j], and since each frame is covered by exactly one
 // token, y_mean[:, j] = attn^T o_mean is a gather of that token's column (exact: one product
@@ -501,7 +505,8 @@ __global__ void __launch_bounds__(256) expand_kernel(ExpandArgs a) {
   const int64_t yl = a.y_len[b];
   const float ym = (int64_t)j < yl ? 1.f : 0.f;
   const float fj = (float)j;
-  // first token with cum > j (cum strictly increases: every w_ceil >= 1)
+  // first token with cum > j (Glow: cum strictly increases, every w_ceil >= 1; VITS: a token with
+  // w_ceil = 0 repeats its predecessor's cum, and the first token past j is the one covering it)
   int l = 0, r = Tx;
   while (l < r) {
     const int mid = (l + r) >> 1;
@@ -515,7 +520,9 @@ __global__ void __launch_bounds__(256) expand_kernel(ExpandArgs a) {
     const float ls = (att != 0.f && a.o_log_scale) ? a.o_log_scale[((size_t)b * C + c) * Tx + i] : 0.f;
     const size_t o = ((size_t)b * C + c) * Ty + j;
     const float nz = a.noise ? a.noise[o] : 0.f;
-    a.z[o] = (mu + expf(ls) * nz * a.noise_scale) * ym;
+    // Glow (glow_tts.py:361): (y_mean + exp(y_log_scale) * noise * noise_scale) * y_mask; VITS
+    // (vits.py:1154): m_p + noise * exp(logs_p) * noise_scale, unmasked
+    a.z[o] = a.vits ? mu + nz * expf(ls) * a.noise_scale : (mu + expf(ls) * nz * a.noise_scale) * ym;
     if (a.y_mean) a.y_mean[o] = mu;
     if (a.y_log_scale) a.y_log_scale[o] = ls;
   }

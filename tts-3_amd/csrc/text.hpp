@@ -3,6 +3,7 @@
 // glow.py:11-67 (prenet), TTS/tts/models/glow_tts.py:342-363 (inference glue).
 #pragma once
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,8 +43,9 @@ void launch_attention(const float* qkv, const float* mask, const float* ek, cons
 // predictor's input cat(x, g.expand(T)) (encoder.py:166-168, masked at duration_predictor.py:66)
 void launch_dp_input(const float* x, const float* g, const float* mask, float* xdp, int B, int H, int Cg, int T,
                      hipStream_t s);
+// vits = 1: the VITS rule (vits.py:1145-1148), w_ceil = ceil(exp(logw) * x_mask * length_scale)
 void launch_durations(const float* logw, const float* xm, float* w_ceil, int64_t* y_len, float* dur, int B, int T,
-                      float length_scale, hipStream_t s);
+                      float length_scale, hipStream_t s, int vits = 0);
 
 struct ExpandArgs {
   const float* w_ceil;       // [B][T_x]
@@ -59,21 +61,39 @@ struct ExpandArgs {
   float* y_mean;             // [B][C][T_y] or NULL
   float* y_log_scale;        // [B][C][T_y] or NULL
   float* attn;               // [B][T_x][T_y] or NULL
+  int vits;                  // 1: z = m_p + noise * exp(logs_p) * noise_scale, unmasked (vits.py:1154)
 };
 void launch_expand(const ExpandArgs& a, int B, hipStream_t s);
 
-std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c);
+// VITS StochasticDurationPredictor pieces (kernels_vits_text.hip)
+// out = gelu(LayerNorm2(sep_conv(x * mask))) (depthwise [C][k], dilation d, zero padding d(k-1)/2)
+void launch_dds_sep_ln_gelu(const float* x, const float* mask, const float* w, const float* bias, const float* gamma,
+                            const float* beta, float* out, int B, int C, int T, int k, int d, hipStream_t s);
+// x += gelu(LayerNorm2(a))
+void launch_dds_ln_gelu_add(const float* a, float* x, const float* gamma, const float* beta, int B, int C, int T,
+                            hipStream_t s);
+void launch_sdp_init(const float* noise, float* z, float noise_scale, int B, int T, hipStream_t s);
+void launch_sdp_affine(float* z, const float* tr, const float* ls, const float* mask, float* logw, int B, int T, int p,
+                       hipStream_t s);
+void launch_sdp_spline(const float* h, float* z, const float* mask, int B, int T, int p, int nb, float tail,
+                       float hscale, hipStream_t s);
+
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp = true);
 void glow_encoder_validate(const TtsGlowEncoderCfg& c);
 
 class GlowEncoder {
  public:
-  GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* host_weights, int device);
+  // with_dp = false: no duration predictor (its weights are absent from host_weights), the VITS
+  // TextEncoder's use of the same RelativePositionTransformer (vits/networks.py:29-100)
+  GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* host_weights, int device, bool with_dp = true);
   ~GlowEncoder();
   GlowEncoder(const GlowEncoder&) = delete;
   GlowEncoder& operator=(const GlowEncoder&) = delete;
   // g: [B][c_in_channels] speaker vector (the reference's g [B][c_in][1]), NULL when c_in_channels == 0
+  // x_out [B][H][T] (may be NULL): the encoder state before the heads (x * x_mask); logw may be NULL
+  // without a duration predictor
   void forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m, float* x_logs,
-               float* logw, float* x_mask, hipStream_t s, Profiler* prof = nullptr);
+               float* logw, float* x_mask, hipStream_t s, Profiler* prof = nullptr, float* x_out = nullptr);
   int device() const { return device_; }
 
  private:
@@ -110,6 +130,7 @@ class GlowEncoder {
 
   TtsGlowEncoderCfg cfg_;
   int device_;
+  bool with_dp_ = true;
   float* emb_ = nullptr;
   Conv pre_conv_[3], pre_proj_;
   Norm pre_norm_[3];
@@ -121,6 +142,76 @@ class GlowEncoder {
   std::vector<TdsLayer> tds_;
   Conv proj_m_, proj_s_, dp1_, dp2_, dp_proj_;
   Norm dpn1_, dpn2_;
+  float* arena_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------
+// VITS text side (vits_text.cpp): TextEncoder on the Glow encoder's transformer, and the
+// StochasticDurationPredictor in the reverse (inference) direction.
+// ---------------------------------------------------------------------------------------
+std::vector<int64_t> vits_text_encoder_weight_shapes(const TtsVitsTextEncoderCfg& c);
+void vits_text_encoder_validate(const TtsVitsTextEncoderCfg& c);
+TtsGlowEncoderCfg vits_text_encoder_glow_cfg(const TtsVitsTextEncoderCfg& c);
+
+class VitsTextEncoder {
+ public:
+  VitsTextEncoder(const TtsVitsTextEncoderCfg& cfg, const float* const* host_weights, int device);
+  void forward(const int64_t* tok, const int64_t* len, int B, int T, float* x, float* m, float* logs, float* x_mask,
+               hipStream_t s, Profiler* prof = nullptr);
+  int device() const { return enc_->device(); }
+
+ private:
+  TtsVitsTextEncoderCfg cfg_;
+  std::unique_ptr<GlowEncoder> enc_;
+};
+
+std::vector<int64_t> vits_sdp_weight_shapes(const TtsVitsSdpCfg& c);
+void vits_sdp_validate(const TtsVitsSdpCfg& c);
+
+class VitsSdp {
+ public:
+  VitsSdp(const TtsVitsSdpCfg& cfg, const float* const* host_weights, int device);
+  ~VitsSdp();
+  VitsSdp(const VitsSdp&) = delete;
+  VitsSdp& operator=(const VitsSdp&) = delete;
+  // logw [B][1][T] = StochasticDurationPredictor(x, x_mask, g, reverse=True, noise_scale) with the
+  // standard normal draw noise [B][2][T] given (stochastic_duration_predictor.py:256-282)
+  void reverse(const float* x, const float* x_mask, const float* g, const float* noise, float noise_scale, int B,
+               int T, float* logw, hipStream_t s, Profiler* prof = nullptr);
+  int device() const { return device_; }
+
+ private:
+  struct Conv {
+    int Cin = 0, Cout = 0, tile = 0, n_chunks = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+  };
+  struct Dds {  // DilatedDepthSeparableConv, 3 layers
+    float* sep_w[3] = {};
+    float* sep_b[3] = {};
+    Conv c1x1[3];
+    float* n1g[3] = {};
+    float* n1b[3] = {};
+    float* n2g[3] = {};
+    float* n2b[3] = {};
+  };
+  struct ConvFlow {
+    Conv pre, proj;
+    Dds dds;
+  };
+  void reserve(int B, int T);
+
+  TtsVitsSdpCfg cfg_;
+  int device_;
+  Conv pre_, proj_;
+  Dds dds_;
+  float* ea_tr_ = nullptr;  // flows.0 (ElementwiseAffine) translation [2], log_scale [2]
+  float* ea_ls_ = nullptr;
+  std::vector<ConvFlow> flows_;  // flows.1 .. flows.num_flows
+  float* cond_w_ = nullptr;      // cond [H][gin], bias [H] (fp32, launch_cond_vec)
+  float* cond_b_ = nullptr;
   float* arena_ = nullptr;
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;

@@ -65,7 +65,10 @@ struct Wino8Cfg {
   static_assert(UPW <= 64 && UNITS <= 256 + 64 && 3 * NCH >= 3, "one transform round per wave; the DMA spreads over 3 steps");
   static_assert(2 * (UNITS - 256) <= 4 * 64, "spread leftover jobs: one per lane of waves 4-7");
   static_assert(TW <= PITCH, "");
-  static_assert(2 * TSZ >= 4 * 16 * PITCH * 4 && 2 * TSZ >= 8 * 8 * 4 * 64 * 4, "epilogue LDS (transformed buffers)");
+  // the transformed buffers double as the epilogue's exchange (8 waves x 8 rows x 64 lanes x 16 B) and
+  // transpose regions; the bf16 scheme's 48-byte rows need the floor
+  static constexpr int EPI = 4 * 16 * PITCH * 4 > 8 * 8 * 4 * 64 * 4 ? 4 * 16 * PITCH * 4 : 8 * 8 * 4 * 64 * 4;
+  static constexpr int TSM = 2 * TSZ > EPI ? 2 * TSZ : EPI;
 };
 
 template <class S, int K, int D, bool LRELU>
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_GAP11
 #define WINO8_GAP11 1
 #endif
-  __shared__ __attribute__((aligned(16))) unsigned char tsm[2 * C::TSZ];  // transformed planes
+  __shared__ __attribute__((aligned(16))) unsigned char tsm[C::TSM];  // transformed planes
   __shared__ __attribute__((aligned(16))) unsigned char rsm[2 * C::RSZ];  // raw input windows
   __shared__ float wbias[128];  // bias + cvec of the 128 rows, staged in the prologue (the epilogue
                                 // reads LDS instead of paying an L2 latency per pass)

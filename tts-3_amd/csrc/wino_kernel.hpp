@@ -88,7 +88,10 @@ struct WinoCfg {
   static constexpr int JSTEP = (NS - JS0) / NJOB > 0 ? (NS - JS0) / NJOB : 1;
   static_assert(J >= 1, "tile narrower than the dilation");
   static constexpr int PITCH = TW <= 128 ? 128 : 256;  // epilogue transpose: samples per LDS row
-  static_assert(TW <= 256 && 2 * XSZB >= 4 * 16 * PITCH * 4, "epilogue transpose: 16 rows per wave in the staging LDS");
+  static_assert(TW <= 256, "epilogue transpose: at most 256 samples per row");
+  // the staging buffers, at least as large as the epilogue transpose (16 rows per wave): the bf16
+  // scheme's 48-byte rows leave 2 XSZB below it
+  static constexpr int SMEM = 2 * XSZB > 4 * 16 * PITCH * 4 ? 2 * XSZB : 4 * 16 * PITCH * 4;
 };
 
 // Epilogue: y = AT . (acc * scale) for the 4 outputs of every (row, tile), then
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(256, TN == 1 ? 2 : 1) void conv1d_wino_kernel(Conv1
   constexpr int NP = S::NP;
   constexpr int NPT = C::NPT;
   constexpr bool H3 = S::SCALED;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;

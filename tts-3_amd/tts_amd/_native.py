@@ -29,7 +29,7 @@ TTS_ERR_OOM = 4
 MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
 # the C-ABI revision these bindings were written for (tts_abi_version() in csrc/abi.cpp)
-ABI_VERSION = 113
+ABI_VERSION = 114
 
 
 def default_math_mode(fp32_faithful_only: bool = True) -> str:
@@ -154,6 +154,32 @@ class TtsVitsPosteriorCfg(Structure):
     ]
 
 
+class TtsVitsTextEncoderCfg(Structure):
+    _fields_ = [
+        ("n_vocab", c_int),
+        ("out_channels", c_int),
+        ("hidden_channels", c_int),
+        ("hidden_channels_ffn", c_int),
+        ("num_heads", c_int),
+        ("num_layers", c_int),
+        ("kernel_size", c_int),
+        ("language_emb_dim", c_int),
+        ("math_mode", c_int),
+    ]
+
+
+class TtsVitsSdpCfg(Structure):
+    _fields_ = [
+        ("in_channels", c_int),
+        ("hidden_channels", c_int),
+        ("kernel_size", c_int),
+        ("num_flows", c_int),
+        ("cond_channels", c_int),
+        ("language_emb_dim", c_int),
+        ("math_mode", c_int),
+    ]
+
+
 class TtsLaunchRecord(Structure):
     _fields_ = [("name", c_char * 48), ("flops", c_double), ("bytes", c_double), ("ms", c_float)]
 
@@ -263,6 +289,38 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
          c_void_p, POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_text_encoder_num_weights": (c_int, [POINTER(TtsVitsTextEncoderCfg)]),
+    "tts_vits_text_encoder_weight_numel": (c_int64, [POINTER(TtsVitsTextEncoderCfg), c_int]),
+    "tts_vits_text_encoder_create": (
+        c_int, [POINTER(TtsVitsTextEncoderCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]
+    ),
+    "tts_vits_text_encoder_destroy": (c_int, [c_void_p]),
+    "tts_vits_text_encoder_forward": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    ),
+    "tts_vits_text_encoder_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_sdp_num_weights": (c_int, [POINTER(TtsVitsSdpCfg)]),
+    "tts_vits_sdp_weight_numel": (c_int64, [POINTER(TtsVitsSdpCfg), c_int]),
+    "tts_vits_sdp_create": (c_int, [POINTER(TtsVitsSdpCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
+    "tts_vits_sdp_destroy": (c_int, [c_void_p]),
+    "tts_vits_sdp_reverse": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_void_p]
+    ),
+    "tts_vits_sdp_reverse_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_durations": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    "tts_vits_expand": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int, c_int,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "tts_op_conv1d": (
         c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
