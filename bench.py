@@ -86,6 +86,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true", help="skip the Glow-TTS + HiFiGAN text->wav measurement")
     p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
     p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
+    p.add_argument("--no-vits-tts", action="store_true", help="skip the VITS tokens -> waveform measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r04.json"))
     p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r04.json"),
                    help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
@@ -154,6 +155,24 @@ def algorithm_ratio(fam_name: str):
         return "direct", 1.0
     K = int(fam_name.split("_k")[1].split("_")[0])
     return "winograd F(4,4)", 7 * ((K + 3) // 4) / 4 / K
+
+
+def family_roofline(rows, mode: str):
+    """The dominant kernel family of one profiled forward against the dense peak of the matrix pipe
+    its arithmetic issues on (the headline's roofline definition, for the side lines)."""
+    name, f, _ = dominant_kernel(rows)
+    algo, ratio = algorithm_ratio(name)
+    avg_ms = f["ms"] / f["n"]
+    exec_flops = f["flops"] / f["n"] * ratio * PRODUCTS[mode]
+    achieved = exec_flops / (avg_ms / 1e3) / 1e12
+    step_ms = sum(r["ms"] for r in rows)
+    return {"bound": "mfma", "kernel": name, "launches": f["n"], "avg_launch_ms": avg_ms, "algorithm": algo,
+            "achieved": achieved, "peak": PIPE_PEAK[mode], "unit": "TFLOP/s", "frac": achieved / PIPE_PEAK[mode],
+            "peak_basis": PIPE_BASIS[mode],
+            "forward_mfma_tflops": sum(r["flops"] * algorithm_ratio(r["name"])[1] * PRODUCTS[mode] for r in rows)
+            / (step_ms / 1e3) / 1e12,
+            "forward_hbm_algorithmic_gbs": sum(r["bytes"] for r in rows) / (step_ms / 1e3) / 1e9,
+            "profiled_forward_ms": step_ms}
 
 
 def cpu_baseline(mel, n_utts: int, pad: int = 5):
@@ -485,10 +504,58 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
             wav = step()
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t0) / steps * 1e3
+        z = flow(zp, mask, g=g, reverse=True) * mask
+        _, rows = dec.profile(z, g=g)
         out["variants"][label] = {"flow_math_mode": fmode, "decoder_math_mode": dmode, "ms_per_step": ms,
                                   "samples_per_s": wav.numel() / (ms / 1e3),
-                                  "rtf": (ms / 1e3) / (wav.numel() / SAMPLE_RATE)}
+                                  "rtf": (ms / 1e3) / (wav.numel() / SAMPLE_RATE),
+                                  "decoder_roofline": family_roofline(rows, dmode)}
         del flow, dec
+    return out
+
+
+def vits_tts_bench(dev, steps=5, warmup=2, B=16, T_x=128):
+    """Vits.inference end to end (vits.py:1088-1174), token ids -> waveform on the device: TextEncoder,
+    StochasticDurationPredictor(reverse), durations, alignment expansion, 4-flow reverse, 512-channel
+    decoder; VitsArgs defaults (LJSpeech VITS: hidden 192, 6 text layers), synthetic weights, both
+    noise draws on the device (inference_noise_scale 0.667, _dp 1.0)."""
+    from tts_amd import synthetic
+    from tts_amd.config import VITS_FLOW, VITS_SDP, VITS_TEXT_ENCODER
+    from tts_amd.tts import Vits
+
+    tok = synthetic.tokens(B, T_x, 64, seed=12).to(dev)
+    lens = torch.full((B,), T_x, dtype=torch.int64, device=dev)
+    out = {"workload": f"Vits.inference, [{B} x {T_x}] token ids -> 22.05 kHz waveform (VitsArgs defaults, "
+                       "512-ch decoder; text encoder + SDP fp32x6)", "variants": {}}
+    for label, (fm, dm) in {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")}.items():
+        v = Vits(dict(num_chars=64), text_math_mode="fp32x6", flow_math_mode=fm, decoder_math_mode=dm)
+        v.text_encoder.load_state_dict(synthetic.vits_text_encoder_state_dict(num_chars=64, **VITS_TEXT_ENCODER))
+        v.duration_predictor.load_state_dict(synthetic.vits_sdp_state_dict(**VITS_SDP, log_duration=1.2))
+        v.flow.load_state_dict(synthetic.vits_flow_state_dict(**VITS_FLOW, seed=2469))
+        v.waveform_decoder.load_state_dict(synthetic.hifigan_state_dict(
+            in_channels=192, out_channels=1, upsample_initial_channel=512, conv_pre_weight_norm=False,
+            conv_post_weight_norm=False, conv_post_bias=False, seed=99, weight_norm=True))
+        v = v.eval().to(dev)
+        gen = torch.Generator(device=dev)
+
+        def step():
+            gen.manual_seed(5)  # the same durations every step (both noise draws pinned)
+            nz_dp = torch.randn(B, 2, T_x, device=dev, generator=gen)
+            return v.inference(tok, {"x_lengths": lens, "noise_dp": nz_dp})
+
+        for _ in range(warmup):
+            o = step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            o = step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        n = o["model_outputs"].numel()
+        out["variants"][label] = {"flow_math_mode": fm, "decoder_math_mode": dm, "ms_per_step": ms,
+                                  "samples_per_s": n / (ms / 1e3), "rtf": (ms / 1e3) / (n / SAMPLE_RATE),
+                                  "mel_frames": int(o["z"].shape[2])}
+        del v
     return out
 
 
@@ -808,6 +875,7 @@ def main():
            if side and not a.no_e2e else None)
     xtts = xtts_decoder_bench(dev, a.math_mode) if side and not a.no_xtts else None
     vits = vits_bench(dev) if side and not a.no_vits else None
+    vits_tts = vits_tts_bench(dev) if side and not a.no_vits_tts else None
 
     if rank == 0:
         rec.update({
@@ -851,6 +919,7 @@ def main():
             "glow_tts_e2e": e2e,
             "xtts_decoder": xtts,
             "vits_waveform": vits,
+            "vits_tts_e2e": vits_tts,
             "accuracy_vs_fp64_oracle": acc,
         })
         emit(rec)

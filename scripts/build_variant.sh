@@ -1,10 +1,11 @@
 # Variant library for A/B runs: the in-tree objects, with the listed translation units rebuilt
-# under DEFS.  usage: bash scripts/build_variant.sh NAME "DEFS" tu1 [tu2 ...]  -> ab/lib_NAME.so
+# under DEFS.  usage: bash scripts/build_variant.sh NAME "DEFS" tu1 [tu2 ...]  -> abx/lib_NAME.so
+# (abx/: the libraries of the A/B session at hand; delete them after it, ab/ is gpurun-ignored)
 set -e
 cd "$(dirname "$0")/../tts-3_amd"
 name=$1; defs=$2; shift 2
 V=build_v_$name
-rm -rf $V && mkdir -p $V && cp build/*.o $V/
+rm -rf $V && mkdir -p $V ../abx && cp build/*.o $V/
 for tu in "$@"; do
   extra=""
   case $tu in kernels_conv_wino|kernels_resblock|kernels_convT_res|kernels_conv_split_h3|kernels_conv_split_b1|kernels_conv_split_x6) extra=-fno-slp-vectorize;; esac
@@ -14,6 +15,6 @@ wait
 printf 'extern "C" const char* tts_build_info(void) { return "target=gfx950 src=variant defs=%s"; }\n' "$(echo $defs | tr ' ' ',')" > $V/build_info.cpp
 /opt/rocm/bin/hipcc -O2 -fPIC -x c++ -c $V/build_info.cpp -o $V/build_info.o
 objs=$(ls build/*.o | sed "s#^build/#$V/#")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,-soname,libtts_mi355x.so -Wl,--no-undefined $objs -o ../ab/lib_$name.so
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,-soname,libtts_mi355x.so -Wl,--no-undefined $objs -o ../abx/lib_$name.so
 rm -rf $V
-echo "ab/lib_$name.so"
+echo "abx/lib_$name.so"

@@ -90,6 +90,30 @@ def test_glow_gate_fusion_bitwise(cuda_device, mode, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("reverse", [True, False])
+def test_glow_wn_update_fusion_bitwise(cuda_device, mode, reverse, monkeypatch):
+    """The WN residual / skip update inside the res_skip conv epilogue (Conv1dArgs::wn_rows, every
+    layer but the last) computes glow_wn_update_kernel's fp32 operations in the same order: bitwise
+    equal outputs (and logdet) with and without it, ragged mask included."""
+    cfg = dict(in_channels=80, hidden_channels=192, kernel_size=5, dilation_rate=1, num_flow_blocks=3,
+               num_coupling_layers=4, num_splits=4, num_squeeze=2)
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(3, 80, 301, generator=g).to(cuda_device)
+    m = (torch.arange(301)[None] < torch.tensor([301, 150, 9])[:, None]).float().unsqueeze(1).to(cuda_device)
+    outs, names = [], []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_FUSION", fused)
+        d = build(cfg, 23, cuda_device, mode)
+        outs.append(d(x, m, reverse=reverse))
+        names.append([r["name"] for r in d.profile(x, m)[1]])
+    assert names[0].count("glow_wn_res_skip_update") == 3 * 3 and names[0].count("glow_wn_update") == 3
+    assert names[1].count("glow_wn_update") == 3 * 4
+    assert torch.equal(outs[0][0], outs[1][0])
+    if not reverse:
+        assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_glow_x0_statistics_match_prepass(cuda_device, monkeypatch):
     """f16x3: every flow's x0 max-abs published by the previous flow's tail kernel equals the
     strided pre-pass it replaced (TTS_MI355X_FLOW_AMAX_PREPASS=1): bitwise equal outputs, ragged

@@ -10,7 +10,7 @@ from _util import assert_close_fp32, goldens, tol
 from oracle import hifigan_ref, vits_ref
 from tts_amd import synthetic
 from tts_amd.config import VITS_DECODER, VITS_FLOW
-from tts_amd.tts import ResidualCouplingBlocks
+from tts_amd.tts import PosteriorEncoder, ResidualCouplingBlocks
 from tts_amd.vocoder import HifiganGenerator
 
 pytestmark = pytest.mark.gpu
@@ -108,6 +108,34 @@ def test_vits_gate_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
         f, _ = build(cfg, 31, cuda_device, mode)
         outs.append(f(x, mask, g=g, reverse=True))
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("cond", [0, 16])
+def test_vits_wn_update_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
+    """The WN residual / skip update inside the res_skip conv epilogue (every layer but the last):
+    bitwise equal to the separate update kernel, in both flow directions and in the posterior
+    encoder's 16-layer WN."""
+    cfg = dict(VITS_FLOW, num_flows=2, cond_channels=cond)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(2, cfg["channels"], 257, generator=gen).to(cuda_device)
+    mask = (torch.arange(257)[None] < torch.tensor([257, 100])[:, None]).float().unsqueeze(1).to(cuda_device)
+    g = torch.randn(2, cond, 1, generator=gen).to(cuda_device) if cond else None
+    spec = torch.randn(2, 64, 257, generator=gen).to(cuda_device)
+    eps = torch.randn(2, 48, 257, generator=gen).to(cuda_device)
+    lens = torch.tensor([257, 100]).to(cuda_device)
+    pcfg = dict(in_channels=64, out_channels=48, hidden_channels=96, kernel_size=5, dilation_rate=1, num_layers=6,
+                cond_channels=cond)
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_FUSION", fused)
+        f, _ = build(cfg, 31, cuda_device, mode)
+        pe = PosteriorEncoder(**pcfg, math_mode=mode)
+        pe.load_state_dict(synthetic.vits_posterior_state_dict(**pcfg, seed=7))
+        pe = pe.to(cuda_device)
+        outs.append((f(x, mask, g=g, reverse=True), f(x, mask, g=g, reverse=False), pe(spec, lens, g=g, noise=eps)[0]))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("cond", [0, 16])

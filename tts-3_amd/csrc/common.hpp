@@ -67,6 +67,11 @@ struct Conv1dArgs {
   int64_t o_bstride;     // floats between batch items of res / y / z (0 = Cout*Tout)
   int64_t cvec_bstride;  // floats between batch items of cvec (0 = Cout)
   int mask_res;          // multiply by mask again after the residual add: (res + v) * mask
+  // wn_rows = H > 0 (split modes, K = 1, H % 32 == 0): the WaveNet res_skip layer's update fused
+  // into the epilogue (wavenet.py:109-113, not the last layer): rows [0, H) update h in place,
+  // y[b][r][t] = (y + v) * mask (y = h, res unused), rows [H, 2H) accumulate the skip sum,
+  // z[b][r - H][t] = v (zmode 1, the first layer) or z + v (zmode 2); amax_out covers h only.
+  int wn_rows;
   // split tile kSplitGateTile only: the WaveNet gate fused into the epilogue (wavenet.py:6-13).
   // gate = H: the packed rows interleave 64-row blocks of the tanh half (rows [0, H)) and the
   // sigmoid half (rows [H, 2H)) (gate_row_order); y receives acts [B][H][Tout] =

@@ -25,8 +25,13 @@ __device__ __forceinline__ float bload(rsrc_t r, unsigned voff, unsigned soff) {
 __device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned voff, unsigned soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
+// cache policy of the activation-plane stores (A/B knob; gfx950 buffer CPol bits: 1 sc0, 2 nt, 16
+// sc1): 0 keeps the written lines in the XCD's L2 (default), sc1 / nt stream them past it
+#ifndef TTS_ST_POL
+#define TTS_ST_POL 0
+#endif
 __device__ __forceinline__ void bstore(rsrc_t r, float v, unsigned voff, unsigned soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, TTS_ST_POL);
 }
 // leaky_relu for 0 < slope <= 1 (slope 1 = identity): max(x, slope*x), 2 VALU
 __device__ __forceinline__ float lrelu2(float x, float slope) { return fmaxf(x, x * slope); }
@@ -158,6 +163,68 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
 }
 
+// WaveNet residual / skip update epilogue (Conv1dArgs::wn_rows, wavenet.py:109-113): the same fp32
+// operations as glow_wn_update_kernel on the conv output v = acc + bias: h = (h + v) * mask for
+// rows < H, skip = v or skip + v for rows >= H.  H % 32 == 0, so a 32-row block is one side.
+template <int TM, int TN, bool AMAX>
+__device__ __forceinline__ void conv_epilogue_wn(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
+                                                 int tbase, int cobase, int lane, const float* sbias, int sbase) {
+  const Conv1dArgs a = args;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int H = a.wn_rows;
+  const int T = a.Tout;
+  const size_t item = (size_t)b * H * T;
+  const unsigned plane = (unsigned)H * (unsigned)T * 4u;
+  const rsrc_t rh = make_rsrc(a.y + item, plane);
+  const rsrc_t rsk = make_rsrc(a.z + item, plane);
+  const rsrc_t rmask = make_rsrc(a.mask + (size_t)b * T, (unsigned)T * 4u);
+  const rsrc_t rbias = make_rsrc(a.bias, (unsigned)(2 * H) * 4u);
+  const bool first = a.zmode == 1;
+  const unsigned rowb = (unsigned)T * 4u;
+  float vmax = 0.f;
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const int rb0 = cobase + m * 32;  // first row of this 32-row block (wave-uniform)
+    if (rb0 >= 2 * H) continue;
+    const bool hrow = rb0 < H;
+    float bv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const unsigned co = (unsigned)(rb0 + (r & 3) + 8 * (r >> 2) + 4 * half);
+      bv[r] = sbias ? sbias[(int)co - sbase] : bload(rbias, co * 4u, 0u);
+    }
+    const rsrc_t rdst = hrow ? rh : rsk;
+    const int prow0 = (hrow ? rb0 : rb0 - H) + 4 * half;  // row in the destination plane
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int t = tbase + n * 32 + l32;
+      const bool tok = t < T;
+      const unsigned voff = tok ? ((unsigned)prow0 * (unsigned)T + (unsigned)t) * 4u : OOB_OFF;
+      const float mv = bload(rmask, tok ? (unsigned)t * 4u : OOB_OFF, 0u);
+      float ov[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ov[r] = (hrow || !first) ? bload(rdst, voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u) : 0.f;
+      float vm = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[m][n][r] + bv[r];
+        float o;
+        if (hrow) {
+          o = (ov[r] + v) * mv;
+          vm = fmaxf(vm, fabsf(o));
+        } else {
+          o = first ? v : ov[r] + v;
+        }
+        bstore(rdst, o, voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb, 0u);
+      }
+      if (AMAX && tok) vmax = fmaxf(vmax, vm);
+    }
+  }
+  if (AMAX && a.amax_out) publish_amax(a.amax_out, b, vmax);
+}
+
 // Polyphase ConvTranspose1d epilogue (Conv1dArgs::ups = U): row rho = co*U + s, column frame m
 // -> y[b][co][U*m + s - U/2].  For U = 8 a lane's registers r = 4i..4i+3 hold the phases
 // 4*half .. 4*half+3 of one channel, i.e. 4 consecutive samples.
@@ -207,7 +274,7 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
             v[j] = (acc[m][n][4 * i + j] + bv[4 * i + j]) + cv[4 * i + j];
             if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v[j]));
           }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)off, 0, TTS_ST_POL);
         }
         continue;
       }
@@ -225,7 +292,7 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
           if (t >= 0 && t + 1 < To) {
             if (AMAX && co < Cr) vmax = fmaxf(vmax, fmaxf(fabsf(v0), fabsf(v1)));
             const f32x2 v = {v0, v1};
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rout, (int)((rowoff + (unsigned)t) * 4u), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rout, (int)((rowoff + (unsigned)t) * 4u), 0, TTS_ST_POL);
           } else {
             const unsigned off0 = (t >= 0 && t < To) ? (rowoff + (unsigned)t) * 4u : OOB_OFF;
             const unsigned off1 = (t + 1 >= 0 && t + 1 < To) ? (rowoff + (unsigned)t + 1u) * 4u : OOB_OFF;

@@ -51,6 +51,15 @@ bool flow_gate_fused(int mode, int H, int K, int dil) {
   return is_split_mode(mode) && H % 64 == 0 && (K == 3 || K == 5 || K == 7) && (K - 1) * dil <= (K - 1) * 5;
 }
 
+bool flow_wn_fused(int mode, int H) {
+  // opt-in (TTS_MI355X_WN_FUSION=1): the res_skip conv's epilogue updates h and the skip sum itself
+  // (Conv1dArgs::wn_rows) for every WN layer but the last.  Measured at config 3 ([16,80,768]):
+  // 22.7 us per fused launch against 14.3 + 8.3 us for the pair, decoder 2.67 vs 2.61 ms: the
+  // epilogue's h / skip gathers after the last MFMA cost what the update kernel did
+  const char* e = std::getenv("TTS_MI355X_WN_FUSION");
+  return (e && e[0] == '1') && is_split_mode(mode) && H % 32 == 0;
+}
+
 bool flow_amax_prepass() {
   const char* e = std::getenv("TTS_MI355X_FLOW_AMAX_PREPASS");
   return e && e[0] == '1';
@@ -123,6 +132,7 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
     : cfg_(cfg), device_(device) {
   glow_validate(cfg_);
   amax_prepass_ = flow_amax_prepass();
+  wn_fused_ = flow_wn_fused(cfg_.math_mode, cfg_.hidden_channels);
   DeviceGuard g(device_);
   const auto shapes = glow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -327,11 +337,22 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
         run(prof, s, "glow_gate", 0.0, 12.0 * P * H,
             [&] { launch_glow_gate(xin, acts, B, H, Th, s, slots(fi, 1 + L + l)); });  // :108
       }
-      conv("glow_wn_res_skip", F.res_skip[l], acts, 0, rs, nullptr, slots(fi, 1 + L + l));  // :109
-      run(prof, s, "glow_wn_update", 0.0, 24.0 * P * H, [&] {
-        launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s,
-                              l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
-      });  // :110-115
+      if (l < L - 1 && wn_fused_) {  // :109-113 in one launch (Conv1dArgs::wn_rows)
+        const Conv& cv = F.res_skip[l];
+        Conv1dArgs a{};
+        a.x = acts; a.w = cv.w; a.bias = cv.b; a.y = hb; a.z = skip; a.mask = msq; a.wn_rows = H;
+        a.amax_in = slots(fi, 1 + L + l); a.amax_out = slots(fi, 2 + l); a.w_exp = cv.w_exp;
+        a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = Th; a.Tout = Th; a.dil = 1; a.pad = 0; a.n_chunks = cv.n_chunks;
+        a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = l == 0 ? 1 : 2; a.zdiv = 1.f;
+        run(prof, s, "glow_wn_res_skip_update", 2.0 * P * cv.Cout * cv.Cin, 4.0 * P * (cv.Cin + 2 * cv.Cout),
+            [&] { launch_conv(cfg_.math_mode, a, B, 1, cv.tile, s); });
+      } else {
+        conv("glow_wn_res_skip", F.res_skip[l], acts, 0, rs, nullptr, slots(fi, 1 + L + l));  // :109
+        run(prof, s, "glow_wn_update", 0.0, 24.0 * P * H, [&] {
+          launch_glow_wn_update(hb, skip, rs, msq, B, H, Th, l == 0, l == L - 1, s,
+                                l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
+        });  // :110-115
+      }
     }
     conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));  // glow.py:214
   };

@@ -39,6 +39,7 @@ int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil);
 // epilogue (kSplitGateTile): split modes, H % 64 == 0, K in {3, 5, 7}, the tile's halo, and
 // TTS_MI355X_FLOW_GATE=1 at create time (opt-in: measured slower end to end at config 3).
 bool flow_gate_fused(int mode, int H, int K, int dil);
+bool flow_wn_fused(int mode, int H);
 // f16x3 statistics of each flow's x0 (the start / pre conv input): by default the previous flow's
 // last writer publishes them (the Glow tail kernel, the VITS post conv epilogue) and only the first
 // flow runs a strided max-abs pre-pass; TTS_MI355X_FLOW_AMAX_PREPASS=1 at create time runs the
@@ -127,6 +128,7 @@ class GlowDecoder {
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;
   bool amax_prepass_ = false;
+  bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
 };
 
 }  // namespace tts

@@ -23,6 +23,8 @@
 // one piece is conflict-free at any tap shift).  leaky_relu before the conv is applied before
 // the split.  One step = (16 input channels, one tap): NP*TM A loads, NP*TN LDS reads,
 // NPROD*TM*TN MFMAs.
+#include <cstdlib>
+#include <string>
 #include <algorithm>
 #include <cstdlib>
 
@@ -104,7 +106,11 @@ int conv1d_split_num_tiles(int mode) {
 int conv1d_split_tile_for(int mode, int Cout, int K, int Cin, int dil, bool res) {
   (void)res;
   if ((K - 1) * dil > (K - 1) * 5) return Cout > 64 ? 0 : (Cout > 32 ? 1 : 2);  // wide-halo tiles
-  if (mode == MATH_FP32_F16X3) {
+  static const bool b1_h3_tiles = [] {  // A/B switch: the bf16 scheme on the f16x3 tile choice
+    const char* e = std::getenv("TTS_MI355X_B1_TILES");
+    return e && std::string(e) == "h3";
+  }();
+  if (mode == MATH_FP32_F16X3 || (mode == MATH_BF16 && b1_h3_tiles)) {
     // ConvTranspose (K == 2) layers included: round-2 re-sweep, DESIGN.md section 4
     if (Cout > 64) return 13;
     if (Cout > 32) return 10;

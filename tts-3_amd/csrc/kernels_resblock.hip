@@ -76,6 +76,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
   __shared__ float red[4];
   __shared__ float bsm[2 * C];  // convs1 and convs2 biases (epilogue reads from LDS, not L2)
+  __shared__ float pws[POST ? C * kPostK : 1];  // POST: conv_post's weights (broadcast reads)
 
   const Conv1dArgs& a1 = pa.c1;
   const int tid = threadIdx.x;
@@ -135,7 +136,8 @@ void resblock_pair_kernel(ResPairArgs pa) {
             v = lrelu2(v, a2.out_slope);
             v = (v + rv[r]) * 1.f;
             v = (zv[r] + v) / a2.zdiv;
-            zt[row * RP_BN + col] = tok ? v : 0.f;
+            // conv_post reads lrelu(z): applied once here instead of once per tap
+            zt[row * RP_BN + col] = tok ? lrelu(v, q.post_slope) : 0.f;
           }
         }
       }
@@ -145,10 +147,11 @@ void resblock_pair_kernel(ResPairArgs pa) {
     const int t = tt0 + col;
     if (col < RP_BN - kPostHalo && t >= 0 && t < T) {
       float o = q.post_bias;
+#pragma unroll 4
       for (int ci = 0; ci < C; ++ci) {
         const float* zr = zt + ci * RP_BN + col - kPostHalo;
 #pragma unroll
-        for (int k = 0; k < kPostK; ++k) o = fmaf(q.post_w[ci * kPostK + k], lrelu(zr[k], q.post_slope), o);
+        for (int k = 0; k < kPostK; ++k) o = fmaf(pws[ci * kPostK + k], zr[k], o);
       }
       q.wav[(size_t)bb * T + t] = tanhf(o);
     }
@@ -255,6 +258,8 @@ void resblock_pair_kernel(ResPairArgs pa) {
     bsm[tid] = bias1;
     bsm[C + tid] = bias2;
   }
+  if constexpr (POST)
+    for (int e = tid; e < C * kPostK; e += 256) pws[e] = pa.post_w[e];
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {

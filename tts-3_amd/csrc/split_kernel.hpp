@@ -310,6 +310,13 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   } else if constexpr (K == 2) {
     convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr, SB ? scvec : nullptr, mt * BM);
   } else {
+    if constexpr (K == 1) {
+      if (a.wn_rows) {
+        conv_epilogue_wn<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr,
+                                     mt * BM);
+        return;
+      }
+    }
     conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, 0x7fffffff, SB ? sbias : nullptr, mt * BM);
   }
 }
@@ -328,6 +335,9 @@ void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
     return;
   }
   TTS_REQUIRE(a.gate == 0, 1, "conv1d(split): the gate epilogue needs tile kSplitGateTile");
+  TTS_REQUIRE(a.wn_rows == 0 || (K == 1 && a.wn_rows % 32 == 0 && a.Cout == 2 * a.wn_rows && a.mask && a.z &&
+                                 a.y && (a.zmode == 1 || a.zmode == 2) && a.ups == 0),
+              1, "conv1d(split): bad WaveNet update-epilogue arguments");
   if (halo <= (K - 1) * 5) {
     hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD>), grid, dim3(256), 0, s, a);
   } else if (WIDE && halo <= 96) {

@@ -66,6 +66,7 @@ void vits_flow_validate(const TtsVitsFlowCfg& c) {
 VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device) : cfg_(cfg), device_(device) {
   vits_flow_validate(cfg_);
   amax_prepass_ = flow_amax_prepass();
+  wn_fused_ = flow_wn_fused(cfg_.math_mode, cfg_.hidden_channels);
   DeviceGuard g(device_);
   const auto shapes = vits_flow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -287,12 +288,23 @@ void VitsFlow::run_flows(bool rev, const float* x, const float* mask, const floa
         run(prof, s, "vits_gate", 0.0, 12.0 * P * H,
             [&] { launch_glow_gate(xin, acts, B, H, T, s, slots(fi, 1 + L + l)); });  // :108
       }
-      conv("vits_wn_res_skip", Fl.res_skip[l], acts, 0, rs, nullptr, nullptr, 0, nullptr, 0, false,
-           slots(fi, 1 + L + l));  // :109
-      run(prof, s, "vits_wn_update", 0.0, 24.0 * P * H, [&] {
-        launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s,
-                              l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
-      });  // :110-115
+      if (l < L - 1 && wn_fused_) {  // :109-113 in one launch (Conv1dArgs::wn_rows)
+        const Conv& cv = Fl.res_skip[l];
+        Conv1dArgs a{};
+        a.x = acts; a.w = cv.w; a.bias = cv.b; a.y = hb; a.z = skip; a.mask = mask; a.wn_rows = H;
+        a.amax_in = slots(fi, 1 + L + l); a.amax_out = slots(fi, 2 + l); a.w_exp = cv.w_exp;
+        a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = T; a.Tout = T; a.dil = 1; a.pad = 0; a.n_chunks = cv.n_chunks;
+        a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = l == 0 ? 1 : 2; a.zdiv = 1.f;
+        run(prof, s, "vits_wn_res_skip_update", 2.0 * P * cv.Cout * cv.Cin, 4.0 * P * (cv.Cin + 2 * cv.Cout),
+            [&] { launch_conv(cfg_.math_mode, a, B, 1, cv.tile, s); });
+      } else {
+        conv("vits_wn_res_skip", Fl.res_skip[l], acts, 0, rs, nullptr, nullptr, 0, nullptr, 0, false,
+             slots(fi, 1 + L + l));  // :109
+        run(prof, s, "vits_wn_update", 0.0, 24.0 * P * H, [&] {
+          launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s,
+                                l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1));
+        });  // :110-115
+      }
     }
     // reverse: x1 = (x1 - post(h) * mask) * mask; forward: x1 = post(h) * mask + x1 * mask; in
     // place on y (networks.py:159-165)
@@ -498,11 +510,22 @@ void VitsPosterior::forward(const float* x, const float* mask, const float* g, c
       run(prof, s, "vits_post_gate", 0.0, 12.0 * P * H,
           [&] { launch_glow_gate(xin, acts, B, H, T, s, slots(1 + L + l)); });
     }
-    conv("vits_post_wn_res_skip", res_skip_[l], acts, rs, nullptr, nullptr, slots(1 + L + l), nullptr);
-    run(prof, s, "vits_post_wn_update", 0.0, 24.0 * P * H, [&] {
-      launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s,
-                            l < L - 1 ? slots(2 + l) : slots(2 * L + 1));
-    });
+    if (l < L - 1 && flow_wn_fused(cfg_.math_mode, H)) {  // :109-113 in one launch (Conv1dArgs::wn_rows)
+      const Conv& cv = res_skip_[l];
+      Conv1dArgs a{};
+      a.x = acts; a.w = cv.w; a.bias = cv.b; a.y = hb; a.z = skip; a.mask = mask; a.wn_rows = H;
+      a.amax_in = slots(1 + L + l); a.amax_out = slots(2 + l); a.w_exp = cv.w_exp;
+      a.Cin = cv.Cin; a.Cout = cv.Cout; a.Tin = T; a.Tout = T; a.dil = 1; a.pad = 0; a.n_chunks = cv.n_chunks;
+      a.in_slope = 1.f; a.out_slope = 1.f; a.zmode = l == 0 ? 1 : 2; a.zdiv = 1.f;
+      run(prof, s, "vits_post_wn_res_skip_update", 2.0 * P * cv.Cout * cv.Cin, 4.0 * P * (cv.Cin + 2 * cv.Cout),
+          [&] { launch_conv(cfg_.math_mode, a, B, 1, cv.tile, s); });
+    } else {
+      conv("vits_post_wn_res_skip", res_skip_[l], acts, rs, nullptr, nullptr, slots(1 + L + l), nullptr);
+      run(prof, s, "vits_post_wn_update", 0.0, 24.0 * P * H, [&] {
+        launch_glow_wn_update(hb, skip, rs, mask, B, H, T, l == 0, l == L - 1, s,
+                              l < L - 1 ? slots(2 + l) : slots(2 * L + 1));
+      });
+    }
   }
   // stats = proj(h) * mask (networks.py:285), then split and sample (:286-287)
   conv("vits_post_proj", proj_, skip, stats, mask, nullptr, slots(2 * L + 1), nullptr);

@@ -54,6 +54,7 @@ class VitsFlow {
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;
   bool amax_prepass_ = false;
+  bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
 };
 
 std::vector<int64_t> vits_posterior_weight_shapes(const TtsVitsPosteriorCfg& c);

@@ -147,7 +147,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // each lane of waves 4-7 takes one (unit, piece pair) job, dealt round-robin over the four waves,
   // so every SIMD runs the transform instructions of one full and one half pass; otherwise wave 4
   // alone takes them whole and its SIMD runs two full passes per chunk while the others run one.
-  constexpr int TG = 0;  // the point group whose waves take the dense units (the DMA waves: slower)
+#ifndef WINO8_TG_B1
+#define WINO8_TG_B1 0
+#endif
+  // the point group whose waves take the dense units (f16x3: group 0; the DMA waves were slower);
+  // bf16 carries a third of the MFMAs, so its balance is measured separately (WINO8_TG_B1)
+  constexpr int TG = S::NP == 1 ? WINO8_TG_B1 : 0;
   const int e = lane * 4 + wm;  // leftover job of a lane of the other group
   const int u = WINO8_DENSE ? (grp == TG ? wm * 64 + lane
                                          : (WINO8_SPREAD ? 256 + (e >> 1) : (wm == 0 ? 256 + lane : C::UNITS)))
@@ -349,6 +354,11 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       lds_sync();
     }
   };
+#ifndef WINO8_PRIO
+#define WINO8_PRIO 0  // A/B: 1 = s_setprio 1 on the DMA waves (4-7) for the main loop, 2 = on waves 0-3
+#endif
+  if (WINO8_PRIO == 1 && grp == 1) __builtin_amdgcn_s_setprio(1);
+  if (WINO8_PRIO == 2 && grp == 0) __builtin_amdgcn_s_setprio(1);
   if (grp == 0) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
 

@@ -146,7 +146,7 @@ __device__ __forceinline__ f32x4 wino_apply(f32x4 y, float bias, float oslope, f
 
 __device__ __forceinline__ void wino_store(const rsrc_t& rout, f32x4 v, unsigned voff, bool full, int nvalid) {
   if (full) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)voff, 0, TTS_ST_POL);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) bstore(rout, v[j], j < nvalid ? voff + 4u * j : OOB_OFF, 0u);

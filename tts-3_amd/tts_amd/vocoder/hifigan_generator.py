@@ -301,19 +301,22 @@ class HifiganGenerator(nn.Module):
         """hifigan_generator.py:267-282: move to the weight device, replicate-pad, forward."""
         return self._run(c, self.inference_padding, g)
 
-    def profile(self, c: torch.Tensor, pad: Optional[int] = None):
-        """One forward with a hipEvent pair around every kernel launch.
-        Returns (wav, [ {name, flops, bytes, ms}, ... ])."""
+    def profile(self, c: torch.Tensor, pad: Optional[int] = None, g: Optional[torch.Tensor] = None):
+        """One forward with a hipEvent pair around every kernel launch (g: the conditioning vector of a
+        cond_channels > 0 generator).  Returns (wav, [ {name, flops, bytes, ms}, ... ])."""
         h = self._native_handle()
         dev = self._device()
         pad = self.inference_padding if pad is None else pad
         x = c.to(device=dev, dtype=torch.float32).contiguous()
         B, C, T = x.shape
+        gg = None
+        if g is not None:
+            gg = g.to(device=dev, dtype=torch.float32).reshape(B, -1).contiguous()
         out = torch.empty(B, self._cfg.out_channels, self.hop_length * (T + 2 * pad), device=dev)
         cap = 4096  # windowed long utterances run ~80 launches per window
         recs = (N.TtsLaunchRecord * cap)()
         n = ctypes.c_int(0)
-        N.call("tts_hifigan_forward_profiled", h, N.ptr(x), B, C, T, pad, None, N.ptr(out),
+        N.call("tts_hifigan_forward_profiled", h, N.ptr(x), B, C, T, pad, N.ptr(gg), N.ptr(out),
                N.stream_ptr(dev), recs, cap, ctypes.byref(n))
         rows = [
             {"name": recs[i].name.decode(), "flops": recs[i].flops, "bytes": recs[i].bytes, "ms": recs[i].ms}
