@@ -87,6 +87,7 @@ def parse():
     p.add_argument("--no-xtts", action="store_true", help="skip the XTTS waveform-decoder measurement")
     p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
     p.add_argument("--no-vits-tts", action="store_true", help="skip the VITS tokens -> waveform measurement")
+    p.add_argument("--no-rb2", action="store_true", help="skip the ResBlock2 (YourTTS decoder) measurement")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r04.json"))
     p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r04.json"),
                    help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
@@ -514,6 +515,58 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
     return out
 
 
+def rb2_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=512):
+    """ResBlock2 generator (hifigan_generator.py:108-159): the YourTTS waveform decoder, i.e. the VITS
+    decoder with resblock_type_decoder "2" (recipes/vctk/yourtts/train_yourtts.py:134; vits.py:704-718:
+    in 192, 512 channels, kernels 3 / 7 / 11 with ResBlock2 dilations (1, 3), speaker cond 512, no
+    conv_post bias, no padding), on [B, 192, T] latents; the whole-block launches against the per-conv
+    path (TTS_MI355X_RESBLOCK3=0) in each math mode."""
+    from tts_amd import synthetic
+    from tts_amd.config import VITS_DECODER
+    from tts_amd.vocoder import HifiganGenerator
+
+    dcfg = dict(VITS_DECODER, cond_channels=cond, resblock_type="2")
+    dsd = synthetic.hifigan_state_dict(**dcfg, seed=77, weight_norm=False)
+    gen = torch.Generator().manual_seed(10)
+    z = torch.randn(B, 192, T, generator=gen).to(dev)
+    g = torch.randn(B, cond, 1, generator=gen).to(dev)
+    out = {"workload": f"YourTTS waveform decoder (HiFiGAN, ResBlock2), [{B}, 192, {T}] latents, speaker cond "
+                       f"{cond}", "variants": {}}
+    prev = os.environ.get("TTS_MI355X_RESBLOCK3")
+    try:
+        for mode in ("f16x3", "bf16"):
+            for fused in (True, False):
+                os.environ["TTS_MI355X_RESBLOCK3"] = "all" if fused else "0"  # read at create
+                dec = HifiganGenerator(**dcfg, math_mode=mode)
+                with contextlib.redirect_stdout(sys.stderr):
+                    dec.remove_weight_norm()
+                dec.load_state_dict(dsd)
+                dec = dec.to(dev)
+                for _ in range(warmup):
+                    wav = dec(z, g=g)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    wav = dec(z, g=g)
+                torch.cuda.synchronize(dev)
+                ms = (time.perf_counter() - t0) / steps * 1e3
+                _, rows = dec.profile(z, g=g)
+                fams = {}
+                for r in rows:
+                    fams[r["name"]] = fams.get(r["name"], 0.0) + r["ms"]
+                out["variants"][f"{mode}_{'whole_block' if fused else 'per_conv'}"] = {
+                    "math_mode": mode, "ms_per_step": ms, "samples_per_s": wav.numel() / (ms / 1e3),
+                    "rtf": (ms / 1e3) / (wav.numel() / SAMPLE_RATE), "decoder_roofline": family_roofline(rows, mode),
+                    "kernel_breakdown_ms": {k: round(v, 3) for k, v in sorted(fams.items(), key=lambda kv: -kv[1])}}
+                del dec
+    finally:
+        if prev is None:
+            os.environ.pop("TTS_MI355X_RESBLOCK3", None)
+        else:
+            os.environ["TTS_MI355X_RESBLOCK3"] = prev
+    return out
+
+
 def vits_tts_bench(dev, steps=5, warmup=2, B=16, T_x=128):
     """Vits.inference end to end (vits.py:1088-1174), token ids -> waveform on the device: TextEncoder,
     StochasticDurationPredictor(reverse), durations, alignment expansion, 4-flow reverse, 512-channel
@@ -876,6 +929,7 @@ def main():
     xtts = xtts_decoder_bench(dev, a.math_mode) if side and not a.no_xtts else None
     vits = vits_bench(dev) if side and not a.no_vits else None
     vits_tts = vits_tts_bench(dev) if side and not a.no_vits_tts else None
+    rb2 = rb2_bench(dev) if side and not a.no_rb2 else None
 
     if rank == 0:
         rec.update({
@@ -920,6 +974,7 @@ def main():
             "xtts_decoder": xtts,
             "vits_waveform": vits,
             "vits_tts_e2e": vits_tts,
+            "resblock2_decoder": rb2,
             "accuracy_vs_fp64_oracle": acc,
         })
         emit(rec)

@@ -13,7 +13,7 @@ for r in 1 2; do
   for v in $AB; do
     name=${v%%:*}; rest=${v#*:}; lib=${rest%%|*}; envs=${rest#*|}; [ "$envs" = "$rest" ] && envs=""
     [ "$lib" = main ] && lib=tts-3_amd/tts_amd/_lib/libtts_mi355x.so
-    env TTS_MI355X_LIB=$lib ${envs//,/ } timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits --no-vits-tts ${AB_BENCH_ARGS} > gpurun_out/ab_${name}_$r.json 2>gpurun_out/ab_${name}_$r.err || exit 1
+    env TTS_MI355X_LIB=$lib ${envs//,/ } timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits --no-vits-tts --no-rb2 ${AB_BENCH_ARGS} > gpurun_out/ab_${name}_$r.json 2>gpurun_out/ab_${name}_$r.err || exit 1
     python -c "
 import json,re;d=json.load(open('gpurun_out/ab_${name}_$r.json'));b=d['kernel_breakdown_ms']
 print('${name}_$r', round(d['ms_per_step'],2), {k: round(v,2) for k,v in b.items() if re.search('${AB_FILTER:-.}', k)})"

@@ -9,7 +9,7 @@ OUT=gpurun_out/prof
 MODE=${PROF_MODE:-f16x3}
 ROUND=${ROUND:-r03}
 mkdir -p $OUT
-BENCH="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits --no-vits-tts --math-mode $MODE"
+BENCH="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits --no-vits-tts --no-rb2 --math-mode $MODE"
 export TTS_FORWARD_NAMES=$OUT/forward_names.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 $BENCH > $OUT/trace.log 2>&1 &&
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- python3 $BENCH > $OUT/fetch.log 2>&1 &&

@@ -441,6 +441,71 @@ def test_whole_block_fusion_matches_unfused(cuda_device, monkeypatch, mode):
     assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)
 
 
+# ResBlock2 topologies at channel widths the whole-block kernel takes (32 / 64 / 128):
+# YourTTS's decoder form (VITS kernels 3, 7, 11 with ResBlock2 dilations (1, 3),
+# recipes/vctk/yourtts/train_yourtts.py:134) and HiFiGAN-v3's kernels / dilations
+RB2_YOURTTS = dict(in_channels=80, out_channels=1, resblock_type="2",
+                   resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5], [1, 3, 5]], resblock_kernel_sizes=[3, 7, 11],
+                   upsample_kernel_sizes=[16, 16, 4, 4], upsample_initial_channel=256, upsample_factors=[8, 8, 2, 2],
+                   inference_padding=5)
+RB2_V3 = dict(in_channels=80, out_channels=1, resblock_type="2",
+              resblock_dilation_sizes=[[1, 2], [2, 6], [3, 12]], resblock_kernel_sizes=[3, 5, 7],
+              upsample_kernel_sizes=[16, 16, 8], upsample_initial_channel=256, upsample_factors=[8, 8, 4],
+              inference_padding=5)
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16", "fp32x6"])
+@pytest.mark.parametrize("topo", ["yourtts", "v3"])
+def test_resblock2_whole_block_matches_unfused(cuda_device, monkeypatch, mode, topo):
+    """ResBlock2 (hifigan_generator.py:108-159) as one launch per block (resblock_block.hpp, kernels
+    3 / 5 / 7 / 11) against the per-conv path (TTS_MI355X_RESBLOCK3=0), both within the mode's gates
+    of the fp64 oracle over several workgroups per utterance, and the fused launches really used."""
+    cfg = RB2_YOURTTS if topo == "yourtts" else RB2_V3
+    sd = synthetic.hifigan_state_dict(seed=43, weight_norm=False, **cfg)
+    mel = synthetic.mel(2, 23, seed=7)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **cfg)
+    outs = []
+    for policy in ("all", "0"):
+        monkeypatch.setenv("TTS_MI355X_RESBLOCK3", policy)
+        g = HifiganGenerator(**cfg, math_mode=mode)
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs.append(g.inference(mel.to(cuda_device)).cpu())
+        names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+        fused = [n for n in names if n.startswith("mrf_block2_")]
+        if policy == "0":
+            assert not fused
+        else:
+            # x6 has no 128-channel form; kernel 7 at dilation 12 (v3) stays per conv
+            # f16x3 / x6 keep kernel 11 at 64 channels per conv (resblock2_preferred)
+            expect = {"yourtts": {"f16x3": 6, "bf16": 7, "fp32x6": 5}, "v3": {"f16x3": 6, "bf16": 6, "fp32x6": 4}}
+            assert len(fused) == expect[topo][mode], names
+        assert_close_fp32(outs[-1], ref, f"{topo} {mode} whole-block={policy}", **tol(mode))
+    assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)
+
+
+@pytest.mark.parametrize("geo64", ["0", "1"])
+def test_resblock2_long_ragged_vs_oracle(cuda_device, monkeypatch, geo64):
+    """The ResBlock2 whole-block kernels at a length spanning many tiles per utterance (and a tile
+    edge that is not a multiple of the column tile) against the fp64 oracle, both 64-channel
+    geometries, every supported block fused (TTS_MI355X_RB2_ALL)."""
+    monkeypatch.setenv("TTS_MI355X_RB2_GEO64", geo64)
+    monkeypatch.setenv("TTS_MI355X_RB2_ALL", "1")
+    cfg = RB2_YOURTTS
+    sd = synthetic.hifigan_state_dict(seed=44, weight_norm=False, **cfg)
+    mel = synthetic.mel(1, 61, seed=8)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **cfg)
+    g = HifiganGenerator(**cfg, math_mode="f16x3")
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    out = g.inference(mel.to(cuda_device)).cpu()
+    assert_close_fp32(out, ref, f"rb2 geo64={geo64}")
+    names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+    assert sum(n.startswith("mrf_block2_") and n.endswith("_c64") for n in names) == 3, names
+
+
 def _padded_slice(mel, pad, a, b):
     """Frames [a, b) of the replicate-padded mel (hifigan_generator.py:281), clamped indices."""
     T = mel.shape[2]

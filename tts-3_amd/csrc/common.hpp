@@ -129,6 +129,13 @@ struct ResBlock3Args {
 };
 bool resblock3_supported(int mode, int C, int K, const int* dil);
 void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s);
+// A whole ResBlock2 (hifigan_generator.py:150-155: two convs of kernel K, dilations dil[0..1],
+// each x = conv(lrelu(x)) + x) in one kernel; ResBlock3Args with w / bias / w_exp[0..1].
+// geo64 = 1: 192-column tiles at C = 64 (default 128)
+bool resblock2_supported(int mode, int C, int K, const int* dil);
+bool resblock2_preferred(int mode, int C, int K, const int* dil);  // supported and measured faster
+int resblock2_geo64(int mode);  // 64-channel tile geometry (TTS_MI355X_RB2_GEO64 overrides)
+void launch_resblock2(int mode, const ResBlock3Args& a, int B, int C, int K, int geo64, hipStream_t s);
 
 // Tile shape of one conv kernel instance (PD: A-operand prefetch distance in steps).
 struct ConvTile {

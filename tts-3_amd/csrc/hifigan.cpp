@@ -107,6 +107,7 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const bool pair_fusion = !(nf && nf[0] == '1');
   const char* pf = std::getenv("TTS_MI355X_POST_FUSION");
   post_fusion_ = !(pf && pf[0] == '0');
+  rb2_geo64_ = resblock2_geo64(mode);
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
@@ -190,12 +191,18 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         }
         rb.fused3 = pair_fusion && tiles_ok;
       } else {
+        bool tiles_ok = true;
         for (int m = 0; m < 2; ++m) {
           rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", true, mode));
           src.push_back({hw[wi], hw[wi + 1]}); wi += 2;
+          // the whole-block kernel reads the direct split packing (not Winograd) as [32-row
+          // block][16-channel group][tap]
+          const ConvTile t = conv_tile(mode, rb.convs[m].tile);
+          tiles_ok = tiles_ok && !t.WINO && t.CK % 16 == 0 && ch % t.CK == 0 && ch % t.BM == 0;
         }
+        rb.fused2 = pair_fusion && tiles_ok;
       }
-      if (cfg_.resblock_type == 1 && rb.fused3) {
+      if (rb.fused2 || (cfg_.resblock_type == 1 && rb.fused3)) {
         // whole-block fusion (kernels_resblock.hip resblock3_kernel): TTS_MI355X_RESBLOCK3 =
         // "0" off, "<C>" blocks of at most C channels, "all" every supported block (default; MI355X
         // A/B scripts/ab_res3.sh: c32 k3 2.52 -> 1.87 ms, c64 k3 3.18 -> 2.93 ms per batch)
@@ -205,7 +212,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
           if (std::string(e) == "all") return 1 << 30;
           return std::atoi(e);
         }();
-        rb.fused3 = ch <= policy && resblock3_supported(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
+        if (cfg_.resblock_type == 1)
+          rb.fused3 = ch <= policy && resblock3_supported(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
+        else
+          rb.fused2 = ch <= policy && resblock2_preferred(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
       }
       res_.push_back(rb);
     }
@@ -617,6 +627,23 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
           conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr,
                slots(gj + 2 * m), last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1));
         }
+      } else if (rb.fused2) {
+        // both convs in one launch: o -> MRF z
+        ResBlock3Args ra{};
+        ra.x = bufO; ra.amax_in = slots(g0);
+        for (int c = 0; c < 2; ++c) {
+          ra.w[c] = rb.convs[c].w; ra.bias[c] = rb.convs[c].b; ra.w_exp[c] = rb.convs[c].w_exp;
+          ra.dil[c] = rb.convs[c].dil;
+        }
+        ra.z = bufZ; ra.zmode = zlast; ra.zdiv = (float)cfg_.num_kernels;
+        ra.amax_out = j == cfg_.num_kernels - 1 ? slots(gz) : nullptr;
+        ra.T = len;
+        const ConvLayer& L1 = rb.convs[0];
+        const double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
+        const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 2.0 * L1.Cout * L1.Cin * L1.K);
+        const std::string nm = "mrf_block2_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
+        run(prof, s, nm.c_str(), flops, bytes,
+            [&] { launch_resblock2(L1.mode, ra, B, L1.Cout, L1.K, rb2_geo64_, s); });
       } else {
         for (int m = 0; m < 2; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;

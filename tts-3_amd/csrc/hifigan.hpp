@@ -102,6 +102,7 @@ class Hifigan {
     std::vector<ConvLayer> convs;  // type 1: c1_0, c2_0, c1_1, c2_1, c1_2, c2_2; type 2: c_0, c_1
     bool fused = false;            // type 1 iterations run as fused convs1 -> convs2 launches
     bool fused3 = false;           // type 1, kernel 3: the whole block in one launch (resblock3)
+    bool fused2 = false;           // type 2: the whole block in one launch (resblock2)
   };
 
   void forward_plain(const float* mel, int B, int C, int T, int pad, const float* g, float* wav, hipStream_t s,
@@ -118,6 +119,7 @@ class Hifigan {
   TtsHifiganCfg cfg_;
   int device_;
   int hop_ = 1;
+  int rb2_geo64_ = 0;         // ResBlock2 at 64 channels: 1 = 192-column tiles (resblock2_geo64)
   bool post_fusion_ = true;  // conv_post inside the last MRF launch (TTS_MI355X_POST_FUSION=0: off)
   ConvLayer pre_;
   std::vector<ConvTLayer> ups_;

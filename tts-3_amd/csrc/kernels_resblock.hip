@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "resblock_block.hpp"
 #include "split_device.hpp"
 
 namespace tts {
@@ -28,9 +29,6 @@ namespace tts {
 //   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
 //   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
 //   instead of 92 KB); the halo costs (K - 1) / 192 of the columns instead of (K - 1) / 256.
-#ifndef RES_STAGE_8R
-#define RES_STAGE_8R 1  // x staging lane map of the pair / whole-block kernels (0: 4 rows x 4 quads)
-#endif
 
 constexpr int kPostK = 7;     // conv_post kernel (hifigan_generator.py:229-230)
 constexpr int kPostHalo = 3;  // its zero-padding halo per side
@@ -461,373 +459,13 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
   TTS_HIP_CHECK(hipGetLastError());
 }
 
-// ---------------------------------------------------------------------------------------
-// Whole kernel-3 ResBlock1 (hifigan_generator.py:84-99, K = 3, dilations d0..d2) in one kernel:
-//   for m in 0..2:  xt = lrelu(convs1[m](lrelu(x)));  x = convs2[m](xt) + x;   z (+)= x
-// All three iterations run on the same RP_W-column grid (column c <-> time t0 - R3_LEAD + c): each
-// conv loses its halo at the grid edges, so the valid columns shrink by d_m + 1 per side per
-// iteration (11 for dilations 1, 3, 5: the first conv reads 5 staged extra columns, the rest only
-// the grid) while the kept ones, [R3_LEAD, RP_W - R3_LEAD), stay exact.  x lives in the
-// accumulator layout in registers (the residual of every iteration), lrelu(x) and xt alternate
-// in one LDS region as split B operands (X rows: column + 5, xt rows: column + 1).  Columns
-// outside the valid range or outside [0, T) are staged as zeros; in the f16x3 scheme the scale of
-// x1, x2 and of every xt is the workgroup's own power of two over its valid columns (exact and
-// batch-invariant), x0 uses its producer's statistics.  One launch replaces three pair launches:
-// x is read once and z written once instead of five C-planes per iteration.
-// ---------------------------------------------------------------------------------------
-constexpr int R3_XOFF = 5;  // X rows hold column + 5 (convs1 halo up to dilation 5)
-// kept columns [R3_LEAD, RP_W - R3_LEAD): only the first conv sees the R3_XOFF staged extra
-// columns, every later one loses d_m (+ 1) columns at the grid edge, 11 for dilations 1, 3, 5
-constexpr int R3_LEAD = 12;
-
-// GEO 0: 256 columns, 4 waves side by side; GEO 1 / 2: 192 / 128 columns, 2 x 2 waves;
-// GEO 3: 128 columns, 8 waves (4 row blocks x 2 column halves at C = 128, two waves per SIMD).
-// Measured (f16x3, per batch): C = 128 GEO 3 5.0 ms vs GEO 2 5.5 ms; 8-wave forms at C = 64
-// (256 columns) and C = 32 (512 columns) were slower than GEO 2 / GEO 0 (+0.2 / +0.3 ms).
-template <class S, int C, int GEO>
-struct Res3Cfg {
-  static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
-  static constexpr int RP_BN = RP_W - 2 * R3_LEAD;
-  static constexpr int NW = GEO == 3 ? 8 : 4;     // waves per workgroup
-  static constexpr int NT = 64 * NW;
-  static constexpr int WN = GEO == 0 ? 4 : 2;
-  static constexpr int WM = NW / WN;
-  static constexpr int TM = C / 32 / WM;
-  static constexpr int TN = RP_W / 32 / WN;
-  static constexpr int NC = C / 16;
-  static constexpr int PR = RP_W + 2 * R3_XOFF;  // rows per group (X: RP_W + 10, xt: RP_W + 2)
-  static constexpr int LDSB = NC * PR * S::ROWB;
-  static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
-};
-
-template <class S, int C, int GEO>
-__global__ __launch_bounds__((Res3Cfg<S, C, GEO>::NT))
-__attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) || GEO == 3 ? 2 : 1)))
-void resblock3_kernel(ResBlock3Args a) {
-  using P = Res3Cfg<S, C, GEO>;
-  constexpr int K = 3;
-  constexpr int NP = S::NP;
-  constexpr bool H3 = S::SCALED;
-  constexpr int TM = P::TM, TN = P::TN, NC = P::NC, PR = P::PR, RP_W = P::RP_W;
-  constexpr int PD = 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
-  constexpr int NT = P::NT;
-  __shared__ float red[2][P::NW];  // double-buffered: consecutive tile_exp calls use different halves
-  __shared__ float bsm[6 * C];  // the six conv biases (read by every epilogue: LDS, not L2, latency)
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int half = lane >> 5;
-  const int l32 = lane & 31;
-  const int wm = __builtin_amdgcn_readfirstlane(wave / P::WN);
-  const int wn = wave % P::WN;
-  const int mrow0 = wm * TM * 32;
-  const int t0 = blockIdx.x * P::RP_BN;
-  const int b = blockIdx.z;
-  const int T = a.T;
-  const int tx0 = t0 - R3_LEAD;  // time of column 0
-  const int xcol0 = wn * TN * 32 + l32;
-  const unsigned avoff = (unsigned)lane * 16u;
-  const unsigned chb = (unsigned)T * 4u;
-  const float* xb = a.x + (size_t)b * C * T;
-  const rsrc_t rx = make_rsrc(xb, (unsigned)C * chb);
-
-  // ---- prologue: lrelu(x0) pieces for columns [-5, RP_W + 5) of every 16-channel group, and x0
-  // itself in the acc layout.  Every load is issued before the first store (one HBM latency for
-  // the whole window instead of one per group: at C = 128 that is 8 groups, 64 VGPRs of window)
-  int ex = H3 ? amax_exp(a.amax_in, b) : 0;
-  f32x16 xr[TM][TN];  // the running residual x (fp32), accumulator layout
-  {
-    const float xs = H3 ? ldexpf(1.f, -ex) : 1.f;
-    constexpr int UG = (PR * 4 + NT - 1) / NT;  // units (row, quad) per group per thread
-    constexpr int BPT = (C + NT - 1) / NT;
-    float bl[6][BPT];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < BPT; ++j) {
-        const int e = tid + j * NT;
-        bl[i][j] = e < C ? a.bias[i][e] : 0.f;
-      }
-    f32x4 xv[NC][UG];
-#pragma unroll
-    for (int g = 0; g < NC; ++g)
-#pragma unroll
-      for (int i = 0; i < UG; ++i) {
-        const int u = tid + i * NT;
-        const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
-        const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
-        const int ts = tx0 - R3_XOFF + r;
-        const bool ok = r < PR && ts >= 0 && ts < T;
-        const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xv[g][i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
-      }
-    // x0 in the acc layout (the residual): the same bytes as the window, so read once the window
-    // has landed (L2 hits; issued together, both missed L2: 2.4x the x plane in FETCH_SIZE).  It is
-    // first needed in conv 1's epilogue, so its latency hides behind conv 1's MFMAs.
-    auto load_xr = [&] {
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          const int t = tx0 + xcol0 + n * 32;
-          const bool tok = t >= 0 && t < T;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
-          }
-        }
-    };
-#pragma unroll
-    for (int g = 0; g < NC; ++g)
-#pragma unroll
-      for (int i = 0; i < UG; ++i) {
-        const int u = tid + i * NT;
-        const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
-        const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
-        if (r < PR) {
-          float v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[j] = lrelu2(xv[g][i][j], 0.1f);
-            if (H3) v[j] *= xs;
-          }
-          split_store4<S>(smem + (g * PR + r) * S::ROWB + 8 * quad_pos(q), v[0], v[1], v[2], v[3]);
-        }
-      }
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads below the window's use
-    load_xr();
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < BPT; ++j) {
-        const int e = tid + j * NT;
-        if (e < C) bsm[i * C + e] = bl[i][j];
-      }
-  }
-  __syncthreads();
-
-  f32x16 acc[TM][TN];
-  f32x4 ar[PD + 1][TM][NP], bcur[TN][NP], bnext[TN][NP];
-  rsrc_t ra[TM];
-  auto conv = [&](int wi, int roff, int kstep) {
-#pragma unroll
-    for (int m = 0; m < TM; ++m) ra[m] = make_rsrc(a.w[wi] + ((size_t)(wm * TM + m) * NC * K) * (NP * 256), 0xFFFFFFFFu);
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n) acc[m][n] = f32x16{};
-#pragma unroll
-    for (int p = 0; p < PD; ++p)
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
-    auto read_b = [&](int g, int k, f32x4 (*dst)[NP]) {
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const unsigned char* pp = smem + (g * PR + xcol0 + n * 32 + roff + k * kstep) * S::ROWB + 16 * half;
-#pragma unroll
-        for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(pp + 32 * q);
-      }
-    };
-    read_b(0, 0, bcur);
-#pragma unroll
-    for (int g = 0; g < NC; ++g) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int st = g * K + k;
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int q = 0; q < NP; ++q)
-            ar[PD][m][q] = bload4(ra[m], avoff, (unsigned)((st + PD) * NP + q) * 1024u);
-        const bool more = (k + 1 < K) || (g + 1 < NC);
-        if (more) read_b((k + 1 < K) ? g : g + 1, (k + 1 < K) ? k + 1 : 0, bnext);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int e = 0; e < S::NPROD; ++e)
-#pragma unroll
-          for (int m = 0; m < TM; ++m)
-#pragma unroll
-            for (int n = 0; n < TN; ++n)
-              acc[m][n] = S::mfma(ar[0][m][S::PA[e]], bcur[n][S::PB[e]], acc[m][n]);
-#pragma unroll
-        for (int p = 0; p < PD; ++p)
-#pragma unroll
-          for (int m = 0; m < TM; ++m)
-#pragma unroll
-            for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
-        if (more) {
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-#pragma unroll
-            for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
-        }
-      }
-    }
-  };
-  // block max of |v| over this workgroup (f16x3 scale exponent); every wave must call it.  The
-  // red halves alternate per call, and the store_pieces barrier between two calls separates a
-  // half's reads from its next writes, so one barrier per call suffices
-  int red_half = 0;
-  auto tile_exp = [&](float vmax) -> int {
-    if (!H3) return 0;
-    vmax = wave_max(vmax);
-    if (lane == 0) red[red_half][wave] = vmax;
-    __syncthreads();  // also: every wave is done reading the LDS region
-    float mx = red[red_half][0];
-#pragma unroll
-    for (int w = 1; w < P::NW; ++w) mx = fmaxf(mx, red[red_half][w]);
-    red_half ^= 1;
-    int e = 0;
-    if (mx > 0.f && mx < INFINITY) {
-      int E;
-      (void)frexpf(mx, &E);
-      e = E - 14;
-    }
-    return e;
-  };
-
-  // acc-layout values (already zeroed where invalid) -> split pieces at LDS row column + roff;
-  // rows of the region outside [roff, roff + RP_W) are zeroed
-  auto store_pieces = [&](int roff, float scale) {
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-#pragma unroll
-        for (int gl = 0; gl < 2; ++gl)
-          store_xt8<S>(smem + (((mrow0 + m * 32) / 16 + gl) * PR + xcol0 + n * 32 + roff) * S::ROWB + 16 * half,
-                       acc[m][n], 8 * gl, scale);
-    // edge rows: [0, roff) and [roff + RP_W, PR) of every group
-    constexpr int EB = 2 * R3_XOFF * S::ROWB;  // upper bound of edge bytes per group
-    for (int e = tid * 16; e < NC * EB; e += NT * 16) {
-      const int g = e / EB;
-      const int o = e - g * EB;  // byte in the edge area: first roff rows, then the tail
-      const int lead_b = roff * S::ROWB;
-      const int tail_b = (PR - roff - RP_W) * S::ROWB;
-      if (o < lead_b) *reinterpret_cast<f32x4*>(smem + g * PR * S::ROWB + o) = f32x4{};
-      else if (o - lead_b < tail_b)
-        *reinterpret_cast<f32x4*>(smem + (g * PR + roff + RP_W) * S::ROWB + (o - lead_b)) = f32x4{};
-    }
-  };
-
-  int lo = -R3_XOFF, hi = RP_W + R3_XOFF;  // valid columns of the staged operand
-#pragma unroll 1
-  for (int it = 0; it < 3; ++it) {
-    const int d = a.dil[it];
-    // ---- convs1[it] on lrelu(x) (X rows = column + 5): taps at column + (k - 1) * d
-    conv(2 * it, R3_XOFF - d, d);
-    lo = max(lo + d, 0);  // outputs exist on the grid [0, RP_W) only
-    hi = min(hi - d, RP_W);
-    {
-      const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it]) : 1.f;
-      const float* bs = bsm + (2 * it) * C;
-      float vmax = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; ++m) {
-        float bv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
-#pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          const int col = xcol0 + n * 32;
-          const int t = tx0 + col;
-          const bool ok = col >= lo && col < hi && t >= 0 && t < T;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float v = lrelu2(acc[m][n][r] * sc + bv[r], 0.1f);
-            v = ok ? v : 0.f;
-            acc[m][n][r] = v;
-            vmax = fmaxf(vmax, fabsf(v));
-          }
-        }
-      }
-      const int et = tile_exp(vmax);
-      if (!H3) __syncthreads();  // every wave done reading X
-      store_pieces(1, H3 ? ldexpf(1.f, -et) : 1.f);  // xt rows = column + 1
-      __syncthreads();
-      ex = et;
-    }
-    // ---- convs2[it] on xt: taps at column + k - 1 = xt rows column + k
-    conv(2 * it + 1, 0, 1);
-    lo += 1;
-    hi -= 1;
-    const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[2 * it + 1]) : 1.f;
-    const float* bs = bsm + (2 * it + 1) * C;
-    if (it < 2) {
-      float vmax = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; ++m) {
-        float bv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
-#pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          const int col = xcol0 + n * 32;
-          const int t = tx0 + col;
-          const bool ok = col >= lo && col < hi && t >= 0 && t < T;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float x1 = (acc[m][n][r] * sc + bv[r]) + xr[m][n][r];  // x = convs2(xt) + x
-            xr[m][n][r] = x1;
-            const float v = ok ? lrelu2(x1, 0.1f) : 0.f;  // the next convs1's operand
-            acc[m][n][r] = v;
-            vmax = fmaxf(vmax, fabsf(v));
-          }
-        }
-      }
-      const int e2 = tile_exp(vmax);
-      if (!H3) __syncthreads();  // every wave done reading xt
-      store_pieces(R3_XOFF, H3 ? ldexpf(1.f, -e2) : 1.f);
-      __syncthreads();
-      ex = e2;
-    } else {
-      // ---- final: x3 = convs2[2](xt) + x2 -> MRF z (kept columns [16, 16 + RP_BN) only)
-      const rsrc_t rz = make_rsrc(a.z + (size_t)b * C * T, (unsigned)C * chb);
-      float vmax = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; ++m) {
-        float bv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bv[r] = bs[mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half];
-#pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          const int col = xcol0 + n * 32;
-          const int t = tx0 + col;
-          const bool keep = col >= R3_LEAD && col < R3_LEAD + P::RP_BN && t >= 0 && t < T;
-          unsigned vo[16];
-          float zv[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            vo[r] = keep ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF;
-            zv[r] = a.zmode >= 2 ? bload(rz, vo[r], 0u) : 0.f;
-          }
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float v = (acc[m][n][r] * sc + bv[r]) + xr[m][n][r];
-            if (a.zmode == 2) v = zv[r] + v;
-            else if (a.zmode == 3) v = (zv[r] + v) / a.zdiv;
-            if (keep) vmax = fmaxf(vmax, fabsf(v));
-            bstore(rz, v, vo[r], 0u);
-          }
-        }
-      }
-      if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
-    }
-  }
-}
 
 namespace {
 template <class S, int C, int GEO>
 void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
-  dim3 grid(ceil_div(a.T, Res3Cfg<S, C, GEO>::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO>), grid, dim3(Res3Cfg<S, C, GEO>::NT), 0, s, a);
+  using P = Res3Cfg<S, C, GEO>;
+  dim3 grid(ceil_div(a.T, P::RP_BN), 1, B);
+  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, 3, 6, R3_XOFF, R3_LEAD>), grid, dim3(P::NT), 0, s, a);
 }
 template <class S>
 void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
@@ -861,6 +499,50 @@ void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_
   if (mode == MATH_FP32_F16X3) launch_res3_s<SchemeH3>(a, B, C, s);
   else if (mode == MATH_BF16) launch_res3_s<SchemeB1>(a, B, C, s);
   else launch_res3_s<SchemeX6>(a, B, C, s);
+  TTS_HIP_CHECK(hipGetLastError());
+}
+
+bool resblock2_supported(int mode, int C, int K, const int* dil) {
+  if (!is_split_mode(mode) || !(K == 3 || K == 5 || K == 7 || K == 11)) return false;
+  if (!(C == 32 || C == 64 || (C == 128 && mode != MATH_FP32_X6 && (K == 3 || K == 5)))) return false;
+  // the valid-range walk: both convs read inside the staged XO columns, the kept columns
+  // [LEAD, RP_W - LEAD) stay inside the valid range
+  const int H = rb2_halo(K), hk = (K - 1) / 2;
+  int lo = -H;
+  for (int m = 0; m < 2; ++m) {
+    if (dil[m] < 1 || hk * dil[m] > H) return false;
+    lo = std::max(lo + hk * dil[m], 0);
+  }
+  return lo <= H;
+}
+
+// Where one launch beats the two per-conv launches (MI355X, YourTTS decoder at 8 x 1024 frames,
+// per forward, whole block vs per conv): f16x3 k3 c64 0.24 vs 0.36 ms, k7 c64 0.42 vs 0.49, k7 c32
+// 0.29 vs 0.42, k11 c32 0.39 vs 0.45, k3 c128 0.41 vs 0.42; bf16 every shape (k11 c64 0.35 vs 0.44).
+// f16x3 k11 c64 is slower fused (0.68 vs 0.59 ms: 30 of 128 columns are halo), and so is its
+// 192-column form (0.75): it stays per conv in the 16-bit-pair split schemes.
+bool resblock2_preferred(int mode, int C, int K, const int* dil) {
+  if (!resblock2_supported(mode, C, K, dil)) return false;
+  const char* e = std::getenv("TTS_MI355X_RB2_ALL");  // tests: every supported block fused
+  if (e && e[0] == '1') return true;
+  return mode == MATH_BF16 || !(C == 64 && K == 11);
+}
+
+// 192-column tiles at 64 channels: bf16 (k11 0.345 vs 0.352 ms, k7 0.272 vs 0.291, k3 0.184 vs
+// 0.195); the split schemes keep 128 (f16x3 k7 0.52 vs 0.42 ms)
+int resblock2_geo64(int mode) {
+  const char* e = std::getenv("TTS_MI355X_RB2_GEO64");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] - '0';
+  return mode == MATH_BF16 ? 1 : 0;
+}
+
+void launch_resblock2(int mode, const ResBlock3Args& a, int B, int C, int K, int geo64, hipStream_t s) {
+  TTS_REQUIRE(resblock2_supported(mode, C, K, a.dil), 3, "resblock2: unsupported configuration");
+  TTS_REQUIRE(a.zmode >= 1 && a.zmode <= 3 && a.z && a.x && a.x != a.z, 1, "resblock2: bad arguments");
+  TTS_REQUIRE((int64_t)C * a.T * 4 < (int64_t(1) << 31), 3, "resblock2: plane exceeds 2 GiB");
+  if (mode == MATH_FP32_F16X3) launch_resblock2_h3(a, B, C, K, geo64, s);
+  else if (mode == MATH_BF16) launch_resblock2_b1(a, B, C, K, geo64, s);
+  else launch_resblock2_x6(a, B, C, K, geo64, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

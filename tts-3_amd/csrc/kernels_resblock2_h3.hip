@@ -1,0 +1,9 @@
+// Whole-ResBlock2 kernels (resblock_block.hpp) for the SchemeH3 split scheme: one compile unit per
+// scheme keeps the build parallel.
+#include "resblock_block.hpp"
+
+namespace tts {
+void launch_resblock2_h3(const ResBlock3Args& a, int B, int C, int K, int geo64, hipStream_t s) {
+  launch_rb2_s<SchemeH3>(a, B, C, K, geo64, s);
+}
+}  // namespace tts
