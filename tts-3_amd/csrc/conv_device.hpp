@@ -33,6 +33,28 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned voff, unsigned soff) 
 __device__ __forceinline__ void bstore(rsrc_t r, float v, unsigned voff, unsigned soff) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, TTS_ST_POL);
 }
+// LDS-DMA of 16 bytes per lane (buffer_load_dwordx4 ... lds: lane l's bytes land at lds + 16 l),
+// issued from inline asm.  With the builtin, the compiler's waitcnt pass makes every later LDS
+// access of the issuing wave wait (vmcnt) until the DMA has landed, whatever buffer it touches, so
+// the wave stalls for an HBM round trip right after each DMA; the callers order the DMA'd data
+// themselves (explicit s_waitcnt vmcnt + barrier before any wave reads it).  Extra vector-memory
+// operations the compiler does not see only make its own vmcnt waits stricter (in-order counter).
+// M0 is reserved: the compiler sets it before each of its own uses, so clobbering it here is safe.
+__device__ __forceinline__ void lds_dma_b128(const void* base, unsigned bytes, unsigned voff, const void* lds) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  // every operand is wave-uniform; readfirstlane puts them in SGPRs (the "s" constraint alone does not)
+  const u32x4_t d = {(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
+                     (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)),
+                     (unsigned)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000u};
+  const unsigned m =
+      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long)(__attribute__((address_space(3))) const void*)lds);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(d), "s"(m)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
 // leaky_relu for 0 < slope <= 1 (slope 1 = identity): max(x, slope*x), 2 VALU
 __device__ __forceinline__ float lrelu2(float x, float slope) { return fmaxf(x, x * slope); }
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }

@@ -90,6 +90,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_PD1
 #define WINO8_PD1 4
 #endif
+#ifndef WINO8_PD11
+#define WINO8_PD11 WINO8_PD  // kernel 11, points 0-3 (A/B: 2 keeps the kernel below 256 VGPRs)
+#endif
 #ifndef WINO8_GAP7
 #define WINO8_GAP7 1
 #endif
@@ -122,6 +125,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // ---- input DMA (waves 4-7): raw[ch][RPITCH] fp32, window start ta = t0 - PAD - ROFF ----
   const int ta = t0 - C::PAD - C::ROFF;
   // DMA instructions i = wm + 4k of raw(c) -> R[rb], for k in [k0, k1) (wave-uniform)
+#ifndef WINO8_ASM_DMA
+#define WINO8_ASM_DMA 1  // 0: the LDS-DMA builtin (the compiler then waits for each DMA at the next LDS access)
+#endif
   auto dma = [&](int c, int rb, int k0 = 0, int k1 = 64) {
     const int c0 = c * 16;
     const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
@@ -129,8 +135,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       const int f = i * 64 + lane;
       const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
       const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
+      if (WINO8_ASM_DMA) {
+        lds_dma_b128(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb, vo, rsm + rb * C::RSZ + i * 1024);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
+      }
     }
   };
 
@@ -275,7 +285,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
     // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
     // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
-    constexpr int PD = P0 > 0 ? WINO8_PD1 : WINO8_PD;
+    constexpr int PD = P0 > 0 ? WINO8_PD1 : (K == 11 ? WINO8_PD11 : WINO8_PD);
     // steps between a transform piece's LDS reads and its math (no later than the next piece's
     // reads); measured per kernel size
     constexpr int GAP0 = K == 11 ? WINO8_GAP11 : WINO8_GAP7;
