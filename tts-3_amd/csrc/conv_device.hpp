@@ -30,6 +30,15 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned voff, unsigned soff) 
 #ifndef TTS_ST_POL
 #define TTS_ST_POL 0
 #endif
+// cache policy of activation-window loads (A/B knob, same CPol bits): 2 (nt) streams them through
+// the L2 with evict-first, so they do not displace the weights every workgroup re-reads
+#ifndef TTS_LDX_POL
+#define TTS_LDX_POL 0
+#endif
+template <int POL = TTS_LDX_POL>
+__device__ __forceinline__ float bload_x(rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, POL));
+}
 __device__ __forceinline__ void bstore(rsrc_t r, float v, unsigned voff, unsigned soff) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, TTS_ST_POL);
 }

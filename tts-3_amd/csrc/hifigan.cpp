@@ -107,6 +107,8 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const bool pair_fusion = !(nf && nf[0] == '1');
   const char* pf = std::getenv("TTS_MI355X_POST_FUSION");
   post_fusion_ = !(pf && pf[0] == '0');
+  const char* ms = std::getenv("TTS_MI355X_MRF_STREAMS");
+  mrf_streams_ = !(ms && ms[0] == '0') && cfg.num_kernels > 1;
   rb2_geo64_ = resblock2_geo64(mode);
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
@@ -309,6 +311,9 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
 
 Hifigan::~Hifigan() {
   DeviceGuard g(device_);
+  for (hipStream_t st : bstream_) (void)hipStreamDestroy(st);
+  for (hipEvent_t e : ev_z_) (void)hipEventDestroy(e);
+  if (ev_ups_) (void)hipEventDestroy(ev_ups_);
   if (arena_) (void)hipFree(arena_);
   if (ws_) (void)hipFree(ws_);
   if (win_) (void)hipFree(win_);
@@ -332,6 +337,24 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
 // max-abs slot groups (fp16 hi/lo mode), [B][64] each: 0 the mel, 1 conv_pre's output, then per
 // stage i from stage_group(i): the upsampled input o, per resblock conv its output
 // (convs1 -> t, convs2 -> x), and the stage's MRF output z/num_kernels
+int Hifigan::n_planes() const { return 2 + 2 * (mrf_streams_ ? cfg_.num_kernels : 1); }
+
+void Hifigan::ensure_branch_streams() {
+  if (!bstream_.empty()) return;
+  // non-blocking: no implicit ordering with the legacy null stream; every dependency is an event
+  for (int j = 1; j < cfg_.num_kernels; ++j) {
+    hipStream_t st;
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    bstream_.push_back(st);
+  }
+  TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_ups_, hipEventDisableTiming));
+  for (int j = 0; j < cfg_.num_kernels; ++j) {
+    hipEvent_t e;
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev_z_.push_back(e);
+  }
+}
+
 int Hifigan::amax_groups() const { return 2 + cfg_.num_upsamples * (2 + cfg_.num_kernels * 6); }
 int Hifigan::stage_group(int i) const { return 2 + i * (2 + cfg_.num_kernels * 6); }
 
@@ -398,7 +421,7 @@ bool Hifigan::windowed(int64_t L) const {
 int64_t Hifigan::plain_workspace_bytes(int B, int64_t L) const {
   const int64_t cond = cond_floats(B);
   const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
-  return (4 * plane_floats(B, (int)L, 0) + cond + amax) * (int64_t)sizeof(float);
+  return (n_planes() * plane_floats(B, (int)L, 0) + cond + amax) * (int64_t)sizeof(float);
 }
 
 int64_t Hifigan::window_buffer_bytes(int B, int64_t W) const {
@@ -482,11 +505,13 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
   const int64_t plane = plane_floats(B, T, pad);
   float* bufZ = ws_;              // conv_pre output, then the MRF sum of each stage
   float* bufO = ws_ + plane;      // upsampled stage input o
-  float* bufX = ws_ + 2 * plane;  // resblock running residual x
-  float* bufT = ws_ + 3 * plane;  // convs1 output (already leaky-relu'd)
-  float* cvec = cfg_.cond_channels > 0 ? ws_ + 4 * plane : nullptr;
+  const int np = n_planes();
+  float* cvec = cfg_.cond_channels > 0 ? ws_ + np * plane : nullptr;
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
-  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + 4 * plane + cond_floats(B)) : nullptr;
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + np * plane + cond_floats(B)) : nullptr;
+  // concurrent MRF branches (not in a profiled forward: its per-launch timings stay serial)
+  const bool conc = mrf_streams_ && prof == nullptr;
+  if (conc) ensure_branch_streams();
   auto slots = [&](int grp) -> unsigned* { return amax ? amax + (size_t)grp * B * 64 : nullptr; };  // [B][64]
   if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, (size_t)amax_groups() * B * 64 * sizeof(unsigned), s));
 
@@ -500,7 +525,8 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
 
   auto conv = [&](const ConvLayer& Ld, const float* x, int Tin, int Tout, int rep, float in_slope,
                   float out_slope, const float* res, float* y, int zmode, const float* cv,
-                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr) {
+                  const unsigned* amax_in = nullptr, unsigned* amax_out = nullptr, hipStream_t st = nullptr) {
+    if (!st) st = s;
     Conv1dArgs a{};
     a.amax_in = amax_in; a.amax_out = amax_out; a.w_exp = Ld.w_exp;
     a.x = x; a.w = Ld.w; a.bias = Ld.b; a.res = res; a.y = y; a.z = bufZ; a.cvec = cv;
@@ -511,7 +537,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
     double bytes = 4.0 * ((double)B * Ld.Cin * Tin + (double)Ld.Cout * Ld.Cin * Ld.K + (double)B * Ld.Cout * Tout);
     if (res) bytes += 4.0 * B * Ld.Cout * (double)Tout;
     if (zmode >= 2) bytes += 4.0 * B * Ld.Cout * (double)Tout;
-    run(prof, s, Ld.name.c_str(), flops, bytes, [&] { launch_conv(Ld.mode, a, B, Ld.K, Ld.tile, s); });
+    run(prof, st, Ld.name.c_str(), flops, bytes, [&] { launch_conv(Ld.mode, a, B, Ld.K, Ld.tile, st); });
   };
 
   // conv_pre on the replicate-padded mel (hifigan_generator.py:281, :249) [+ cond_layer(g), :250-251]
@@ -555,9 +581,22 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
       run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_convT(ta, B, U.U, U.tile, s); });
     }
     len = lout;
+    if (conc) TTS_HIP_CHECK(hipEventRecord(ev_ups_, s));  // o is ready for every branch
     // MRF: z = sum_j resblock_j(o); o = z / num_kernels (:255-261)
     for (int j = 0; j < cfg_.num_kernels; ++j) {
       const ResBlock& rb = res_[i * cfg_.num_kernels + j];
+      // branch j: its stream and its own X / T planes when the branches run concurrently
+      const hipStream_t sj = conc && j > 0 ? bstream_[j - 1] : s;
+      float* bufX = ws_ + (2 + 2 * (conc ? j : 0)) * plane;  // resblock running residual x
+      float* bufT = bufX + plane;                            // convs1 output (already leaky-relu'd)
+      if (conc && j > 0) TTS_HIP_CHECK(hipStreamWaitEvent(sj, ev_ups_, 0));
+      // the MRF-sum writer of branch j reads the z branch j - 1 wrote: keep that order
+      auto zorder = [&] {
+        if (conc && j > 0) TTS_HIP_CHECK(hipStreamWaitEvent(sj, ev_z_[j - 1], 0));
+      };
+      auto zdone = [&] {
+        if (conc) TTS_HIP_CHECK(hipEventRecord(ev_z_[j], sj));
+      };
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
       const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
       const int gz = g0 + 1 + cfg_.num_kernels * 6;  // the stage's z / num_kernels
@@ -574,7 +613,9 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         const double flops = 12.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
         const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 6.0 * L1.Cout * L1.Cin * L1.K);
         const std::string nm = "mrf_block_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
-        run(prof, s, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, s); });
+        zorder();
+        run(prof, sj, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, sj); });
+        zdone();
       } else if (cfg_.resblock_type == 1 && rb.fused) {
         // x_{m+1} = convs2[m](lrelu(convs1[m](lrelu(x_m)))) + x_m in one launch per m; the
         // iterates ping-pong between X and T (o -> X -> T -> X / the MRF z)
@@ -614,7 +655,9 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
           }
           const std::string nm = std::string(post ? "mrf_pair_post_k" : "mrf_pair_k") + std::to_string(L1.K) +
                                  "_c" + std::to_string(L1.Cout);
-          run(prof, s, nm.c_str(), flops, bytes, [&] { launch_resblock_pair(L1.mode, pa, B, L1.K, L1.Cout, s); });
+          if (last) zorder();
+          run(prof, sj, nm.c_str(), flops, bytes, [&] { launch_resblock_pair(L1.mode, pa, B, L1.K, L1.Cout, sj); });
+          if (last) zdone();
         }
       } else if (cfg_.resblock_type == 1) {
         for (int m = 0; m < 3; ++m) {
@@ -622,10 +665,13 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
           const unsigned* xin_amax = (m == 0) ? slots(g0) : slots(gj + 2 * m - 1);
           const bool last = (m == 2);
           // xt = convs1[m](lrelu(x)); xt = lrelu(xt)       (ResBlock1.forward :94-96)
-          conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr, xin_amax, slots(gj + 2 * m));
+          conv(rb.convs[2 * m], xin, len, len, 0, 0.1f, 0.1f, nullptr, bufT, 0, nullptr, xin_amax, slots(gj + 2 * m),
+               sj);
           // x = convs2[m](xt) + x                          (:97-98)
+          if (last) zorder();
           conv(rb.convs[2 * m + 1], bufT, len, len, 0, 1.f, 1.f, xin, bufX, last ? zlast : 0, nullptr,
-               slots(gj + 2 * m), last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1));
+               slots(gj + 2 * m), last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1), sj);
+          if (last) zdone();
         }
       } else if (rb.fused2) {
         // both convs in one launch: o -> MRF z
@@ -642,19 +688,25 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         const double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
         const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 2.0 * L1.Cout * L1.Cin * L1.K);
         const std::string nm = "mrf_block2_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
-        run(prof, s, nm.c_str(), flops, bytes,
-            [&] { launch_resblock2(L1.mode, ra, B, L1.Cout, L1.K, rb2_geo64_, s); });
+        zorder();
+        run(prof, sj, nm.c_str(), flops, bytes,
+            [&] { launch_resblock2(L1.mode, ra, B, L1.Cout, L1.K, rb2_geo64_, sj); });
+        zdone();
       } else {
         for (int m = 0; m < 2; ++m) {
           const float* xin = (m == 0) ? bufO : bufX;
           const unsigned* xin_amax = (m == 0) ? slots(g0) : slots(gj + m - 1);
           const bool last = (m == 1);
           // x = convs[m](lrelu(x)) + x                     (ResBlock2.forward :151-154)
+          if (last) zorder();
           conv(rb.convs[m], xin, len, len, 0, 0.1f, 1.f, xin, bufX, last ? zlast : 0, nullptr, xin_amax,
-               last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + m));
+               last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + m), sj);
+          if (last) zdone();
         }
       }
     }
+    // the stage's z (and every branch before it) is complete before the next stage's ups
+    if (conc) TTS_HIP_CHECK(hipStreamWaitEvent(s, ev_z_[cfg_.num_kernels - 1], 0));
     cur = bufZ;
   }
   // leaky_relu (default slope 0.01!) -> conv_post -> tanh (:262-264)

@@ -115,12 +115,21 @@ class Hifigan {
   int64_t cond_floats(int B) const;
   int amax_groups() const;
   int stage_group(int i) const;
+  int n_planes() const;  // activation planes of the workspace (Z, O, then X / T per branch)
+  void ensure_branch_streams();
 
   TtsHifiganCfg cfg_;
   int device_;
   int hop_ = 1;
   int rb2_geo64_ = 0;         // ResBlock2 at 64 channels: 1 = 192-column tiles (resblock2_geo64)
   bool post_fusion_ = true;  // conv_post inside the last MRF launch (TTS_MI355X_POST_FUSION=0: off)
+  // MRF branches on concurrent streams (TTS_MI355X_MRF_STREAMS=0: one stream): branch j > 0 runs
+  // on bstream_[j - 1], each branch with its own X / T planes; the branches' final (MRF-sum)
+  // launches stay in order j = 0, 1, ... through events, so z = ((r0 + r1) + r2) / 3 as before
+  bool mrf_streams_ = true;
+  std::vector<hipStream_t> bstream_;
+  hipEvent_t ev_ups_ = nullptr;
+  std::vector<hipEvent_t> ev_z_;
   ConvLayer pre_;
   std::vector<ConvTLayer> ups_;
   std::vector<ResBlock> res_;

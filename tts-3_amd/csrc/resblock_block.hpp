@@ -27,6 +27,9 @@ namespace tts {
 // ResBlock1 k3: X rows hold column + 5 (convs1 halo up to dilation 5); kept columns
 // [R3_LEAD, RP_W - R3_LEAD): only the first conv sees the R3_XOFF staged extra columns, every
 // later one loses d_m (+ 1) columns at the grid edge, 11 for dilations 1, 3, 5
+#ifndef R3_XR_POL
+#define R3_XR_POL 0  // cache policy of the residual re-read (A/B)
+#endif
 constexpr int R3_XOFF = 5;
 constexpr int R3_LEAD = 12;
 // ResBlock2 kernel K: XO = LEAD = (K - 1) / 2 * the largest dilation it takes (K 3: 4, K 5: 6,
@@ -115,7 +118,7 @@ void resblock3_kernel(ResBlock3Args a) {
         const bool ok = r < PR && ts >= 0 && ts < T;
         const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[g][i][j] = bload(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
+        for (int j = 0; j < 4; ++j) xv[g][i][j] = bload_x(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
       }
     // x0 in the acc layout (the residual): the same bytes as the window, so read once the window
     // has landed (L2 hits; issued together, both missed L2: 2.4x the x plane in FETCH_SIZE).  It is
@@ -130,7 +133,7 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            xr[m][n][r] = bload(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+            xr[m][n][r] = bload_x<R3_XR_POL>(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
           }
         }
     };
