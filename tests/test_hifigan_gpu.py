@@ -605,3 +605,32 @@ def test_conv_post_fusion_bitwise(cuda_device, monkeypatch, mode):
             names = [r["name"] for r in g.profile(mel)[1]]
             assert ("conv_post" in names) == (fused == "0"), names[-3:]
         assert torch.equal(outs["1"], outs["0"]), (B, T, (outs["1"] - outs["0"]).abs().max().item())
+
+
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
+def test_concurrent_schedules_bitwise(cuda_device, monkeypatch, mode):
+    """Execution lanes (Hifigan::forward): the MRF branches on 1, 2 or 3 streams
+    (TTS_MI355X_MRF_STREAMS) and the batch split into sub-batches on concurrent lanes
+    (TTS_MI355X_SUBBATCH, uneven at B = 5) compute every utterance with the same kernels in the
+    same order, so the waveforms are bitwise those of the one-stream forward; and the result is
+    still the reference generator's (fp64 oracle, the mode's gate)."""
+    sd = synthetic.hifigan_state_dict(seed=71, weight_norm=False)
+    mel = synthetic.mel(5, 40, seed=72)
+    outs = {}
+    for streams, sub in (("1", "1"), (None, None), ("3", "1"), ("2", "2"), ("3", "3"), ("3", "8")):
+        for var, val in (("TTS_MI355X_MRF_STREAMS", streams), ("TTS_MI355X_SUBBATCH", sub)):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)  # the defaults
+            else:
+                monkeypatch.setenv(var, val)
+        g = HifiganGenerator(**V1, math_mode=mode)
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs[(streams, sub)] = g.inference(mel.to(cuda_device)).cpu()
+        outs[(streams, sub, 2)] = g.inference(mel.to(cuda_device)).cpu()  # reused lanes / events
+    base = outs[("1", "1")]
+    for k, v in outs.items():
+        assert torch.equal(v, base), f"schedule {k} differs from the one-stream forward ({mode})"
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    assert_close_fp32(base, ref, f"concurrent schedules ({mode})", **tol(mode))

@@ -108,7 +108,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const char* pf = std::getenv("TTS_MI355X_POST_FUSION");
   post_fusion_ = !(pf && pf[0] == '0');
   const char* ms = std::getenv("TTS_MI355X_MRF_STREAMS");
-  mrf_streams_ = !(ms && ms[0] == '0') && cfg.num_kernels > 1;
+  nbs_ = ms ? std::max(1, std::min(std::atoi(ms), cfg.num_kernels)) : cfg.num_kernels;
+  nbs_env_ = ms != nullptr;
+  const char* sb = std::getenv("TTS_MI355X_SUBBATCH");
+  n_lanes_ = sb ? std::max(1, std::min(std::atoi(sb), 8)) : 2;
   rb2_geo64_ = resblock2_geo64(mode);
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
@@ -311,9 +314,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
 
 Hifigan::~Hifigan() {
   DeviceGuard g(device_);
-  for (hipStream_t st : bstream_) (void)hipStreamDestroy(st);
-  for (hipEvent_t e : ev_z_) (void)hipEventDestroy(e);
-  if (ev_ups_) (void)hipEventDestroy(ev_ups_);
+  for (Lane& ln : lanes_) {
+    for (hipStream_t st : ln.branch) (void)hipStreamDestroy(st);
+    if (ln.own) (void)hipStreamDestroy(ln.own);
+    for (hipEvent_t e : ln.ev_z) (void)hipEventDestroy(e);
+    if (ln.ev_ups) (void)hipEventDestroy(ln.ev_ups);
+    if (ln.ev_done) (void)hipEventDestroy(ln.ev_done);
+  }
+  if (ev_start_) (void)hipEventDestroy(ev_start_);
   if (arena_) (void)hipFree(arena_);
   if (ws_) (void)hipFree(ws_);
   if (win_) (void)hipFree(win_);
@@ -337,22 +345,37 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
 // max-abs slot groups (fp16 hi/lo mode), [B][64] each: 0 the mel, 1 conv_pre's output, then per
 // stage i from stage_group(i): the upsampled input o, per resblock conv its output
 // (convs1 -> t, convs2 -> x), and the stage's MRF output z/num_kernels
-int Hifigan::n_planes() const { return 2 + 2 * (mrf_streams_ ? cfg_.num_kernels : 1); }
+int Hifigan::n_planes() const { return 2 + 2 * nbs_; }
 
-void Hifigan::ensure_branch_streams() {
-  if (!bstream_.empty()) return;
-  // non-blocking: no implicit ordering with the legacy null stream; every dependency is an event
-  for (int j = 1; j < cfg_.num_kernels; ++j) {
+void Hifigan::ensure_lanes() {
+  if (!lanes_.empty()) return;
+  auto stream = [] {
+    // non-blocking: no implicit ordering with the legacy null stream; every dependency is an event
     hipStream_t st;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    bstream_.push_back(st);
-  }
-  TTS_HIP_CHECK(hipEventCreateWithFlags(&ev_ups_, hipEventDisableTiming));
-  for (int j = 0; j < cfg_.num_kernels; ++j) {
+    return st;
+  };
+  auto event = [] {
     hipEvent_t e;
     TTS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ev_z_.push_back(e);
+    return e;
+  };
+  lanes_.resize(n_lanes_);
+  for (int i = 0; i < n_lanes_; ++i) {
+    Lane& ln = lanes_[i];
+    if (i > 0) ln.own = stream();
+    for (int j = 1; j < nbs_; ++j) ln.branch.push_back(stream());
+    ln.ev_ups = event();
+    ln.ev_done = event();
+    for (int j = 0; j < cfg_.num_kernels; ++j) ln.ev_z.push_back(event());
   }
+  ev_start_ = event();
+}
+
+int64_t Hifigan::lane_bytes(int B, int64_t L) const {
+  const int64_t cond = cond_floats(B);
+  const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
+  return ((n_planes() * plane_floats(B, (int)L, 0) + cond + amax + 63) / 64 * 64) * (int64_t)sizeof(float);
 }
 
 int Hifigan::amax_groups() const { return 2 + cfg_.num_upsamples * (2 + cfg_.num_kernels * 6); }
@@ -419,9 +442,10 @@ bool Hifigan::windowed(int64_t L) const {
 }
 
 int64_t Hifigan::plain_workspace_bytes(int B, int64_t L) const {
-  const int64_t cond = cond_floats(B);
-  const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
-  return (n_planes() * plane_floats(B, (int)L, 0) + cond + amax) * (int64_t)sizeof(float);
+  // one region for the whole batch (profiled and windowed forwards), or one per lane
+  int64_t lanes = 0;
+  for (int i = 0; i < n_lanes_; ++i) lanes += lane_bytes(lane_batch(B, i), L);
+  return std::max(lane_bytes(B, L), lanes);
 }
 
 int64_t Hifigan::window_buffer_bytes(int B, int64_t W) const {
@@ -471,7 +495,41 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
   TTS_REQUIRE(cfg_.cond_channels == 0 || gvec != nullptr, 1, "cond_channels > 0 requires g");
   const int64_t L = (int64_t)T + 2 * pad;
   if (!windowed(L)) {
-    forward_plain(mel, B, C, T, pad, gvec, wav, s, prof);
+    DeviceGuard dg(device_);
+    reserve_plain(B, L);
+    // a profiled forward stays on one stream (its per-launch timings are serial)
+    if (prof) {
+      forward_plain(mel, B, C, T, pad, gvec, wav, s, prof, ws_, nullptr);
+      return;
+    }
+    ensure_lanes();
+    const int nl = std::min(n_lanes_, B);
+    // split batches run one stream per lane unless TTS_MI355X_MRF_STREAMS says otherwise
+    for (Lane& ln : lanes_) ln.nbs = (nl > 1 && !nbs_env_) ? 1 : nbs_;
+    if (nl == 1) {
+      forward_plain(mel, B, C, T, pad, gvec, wav, s, nullptr, ws_, &lanes_[0]);
+      return;
+    }
+    // sub-batches on concurrent lanes: lane 0 on the caller's stream, lane i > 0 on its own stream
+    // after everything enqueued on s so far; s waits for every lane at the end
+    TTS_HIP_CHECK(hipEventRecord(ev_start_, s));
+    float* ws = ws_;
+    int b0 = 0;
+    for (int i = 0; i < nl; ++i) {
+      const int Bi = lane_batch(B, i);
+      Lane& ln = lanes_[i];
+      const hipStream_t si = i == 0 ? s : ln.own;
+      if (i > 0) TTS_HIP_CHECK(hipStreamWaitEvent(si, ev_start_, 0));
+      forward_plain(mel + (int64_t)b0 * C * T, Bi, C, T, pad,
+                    gvec ? gvec + (int64_t)b0 * cfg_.cond_channels : nullptr, wav + (int64_t)b0 * out_len(T, pad), si,
+                    nullptr, ws, &ln);
+      if (i > 0) {
+        TTS_HIP_CHECK(hipEventRecord(ln.ev_done, si));
+        TTS_HIP_CHECK(hipStreamWaitEvent(s, ln.ev_done, 0));
+      }
+      ws += lane_bytes(Bi, L) / (int64_t)sizeof(float);
+      b0 += Bi;
+    }
     return;
   }
   DeviceGuard dg(device_);
@@ -489,7 +547,11 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     // melw[b][c][t] = replicate_pad(mel)[b][c][w0 + t]  (hifigan_generator.py:281)
     run(prof, s, "mel_window", 0.0, 8.0 * B * C * (double)W,
         [&] { launch_mel_window(mel, B, C, T, pad, w0, W, melw, s); });
-    forward_plain(melw, B, C, W, 0, gvec, outw, s, prof);
+    if (!prof) {
+      ensure_lanes();
+      lanes_[0].nbs = nbs_;
+    }
+    forward_plain(melw, B, C, W, 0, gvec, outw, s, prof, ws_, prof ? nullptr : &lanes_[0]);
     // the payload's samples: outw[b][hop*(s0-w0) ...) -> wav[b][hop*s0 ...)
     TTS_HIP_CHECK(hipMemcpy2DAsync(wav + hop_ * s0, sizeof(float) * hop_ * L, outw + hop_ * (s0 - w0),
                                    sizeof(float) * hop_ * W, sizeof(float) * hop_ * (s1 - s0), B,
@@ -498,20 +560,21 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
 }
 
 void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, const float* gvec, float* wav,
-                            hipStream_t s, Profiler* prof) {
+                            hipStream_t s, Profiler* prof, float* ws, Lane* lane) {
   DeviceGuard g(device_);
-  reserve_plain(B, (int64_t)T + 2 * pad);
 
   const int64_t plane = plane_floats(B, T, pad);
-  float* bufZ = ws_;              // conv_pre output, then the MRF sum of each stage
-  float* bufO = ws_ + plane;      // upsampled stage input o
+  float* bufZ = ws;               // conv_pre output, then the MRF sum of each stage
+  float* bufO = ws + plane;       // upsampled stage input o
   const int np = n_planes();
-  float* cvec = cfg_.cond_channels > 0 ? ws_ + np * plane : nullptr;
+  float* cvec = cfg_.cond_channels > 0 ? ws + np * plane : nullptr;
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
-  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws_ + np * plane + cond_floats(B)) : nullptr;
-  // concurrent MRF branches (not in a profiled forward: its per-launch timings stay serial)
-  const bool conc = mrf_streams_ && prof == nullptr;
-  if (conc) ensure_branch_streams();
+  unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws + np * plane + cond_floats(B)) : nullptr;
+  // concurrent MRF branches (a lane with more than one stream; never in a profiled forward)
+  const int nbs = lane ? lane->nbs : 1;
+  const bool conc = nbs > 1;
+  const int K = cfg_.num_kernels;
+  auto bstream = [&](int j) { return std::max(0, j - (K - nbs)); };  // branch j -> stream index
   auto slots = [&](int grp) -> unsigned* { return amax ? amax + (size_t)grp * B * 64 : nullptr; };  // [B][64]
   if (h3) TTS_HIP_CHECK(hipMemsetAsync(amax, 0, (size_t)amax_groups() * B * 64 * sizeof(unsigned), s));
 
@@ -581,21 +644,22 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
       run(prof, s, U.name.c_str(), uflops, ubytes, [&] { launch_convT(ta, B, U.U, U.tile, s); });
     }
     len = lout;
-    if (conc) TTS_HIP_CHECK(hipEventRecord(ev_ups_, s));  // o is ready for every branch
+    if (conc) TTS_HIP_CHECK(hipEventRecord(lane->ev_ups, s));  // o is ready for every branch
     // MRF: z = sum_j resblock_j(o); o = z / num_kernels (:255-261)
-    for (int j = 0; j < cfg_.num_kernels; ++j) {
-      const ResBlock& rb = res_[i * cfg_.num_kernels + j];
-      // branch j: its stream and its own X / T planes when the branches run concurrently
-      const hipStream_t sj = conc && j > 0 ? bstream_[j - 1] : s;
-      float* bufX = ws_ + (2 + 2 * (conc ? j : 0)) * plane;  // resblock running residual x
-      float* bufT = bufX + plane;                            // convs1 output (already leaky-relu'd)
-      if (conc && j > 0) TTS_HIP_CHECK(hipStreamWaitEvent(sj, ev_ups_, 0));
+    for (int j = 0; j < K; ++j) {
+      const ResBlock& rb = res_[i * K + j];
+      // branch j: its stream and that stream's X / T planes
+      const int bj = conc ? bstream(j) : 0;
+      const hipStream_t sj = bj > 0 ? lane->branch[bj - 1] : s;
+      float* bufX = ws + (2 + 2 * bj) * plane;  // resblock running residual x
+      float* bufT = bufX + plane;               // convs1 output (already leaky-relu'd)
+      if (bj > 0) TTS_HIP_CHECK(hipStreamWaitEvent(sj, lane->ev_ups, 0));
       // the MRF-sum writer of branch j reads the z branch j - 1 wrote: keep that order
       auto zorder = [&] {
-        if (conc && j > 0) TTS_HIP_CHECK(hipStreamWaitEvent(sj, ev_z_[j - 1], 0));
+        if (bj > 0 && bstream(j - 1) != bj) TTS_HIP_CHECK(hipStreamWaitEvent(sj, lane->ev_z[j - 1], 0));
       };
       auto zdone = [&] {
-        if (conc) TTS_HIP_CHECK(hipEventRecord(ev_z_[j], sj));
+        if (conc) TTS_HIP_CHECK(hipEventRecord(lane->ev_z[j], sj));
       };
       const int zlast = (cfg_.num_kernels == 1 || j == 0) ? 1 : (j == cfg_.num_kernels - 1 ? 3 : 2);
       const int gj = g0 + 1 + j * 6;  // slot group of conv c of this resblock: gj + c
@@ -706,7 +770,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
       }
     }
     // the stage's z (and every branch before it) is complete before the next stage's ups
-    if (conc) TTS_HIP_CHECK(hipStreamWaitEvent(s, ev_z_[cfg_.num_kernels - 1], 0));
+    if (conc && bstream(K - 1) > 0) TTS_HIP_CHECK(hipStreamWaitEvent(s, lane->ev_z[K - 1], 0));
     cur = bufZ;
   }
   // leaky_relu (default slope 0.01!) -> conv_post -> tanh (:262-264)

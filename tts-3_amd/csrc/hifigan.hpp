@@ -105,8 +105,24 @@ class Hifigan {
     bool fused2 = false;           // type 2: the whole block in one launch (resblock2)
   };
 
+  // Execution lanes: the batch may split into n_lanes_ sub-batches (TTS_MI355X_SUBBATCH), each a
+  // complete forward on its own workspace region and streams (utterances are independent and every
+  // kernel is batch-invariant, so the output is bitwise the same); within a lane the MRF branches
+  // spread over nbs_ streams (TTS_MI355X_MRF_STREAMS, default one per branch): branch j runs on
+  // stream max(0, j - (num_kernels - nbs_)), each stream with its own X / T planes; the branches'
+  // MRF-sum launches stay in order j = 0, 1, ... through events, so z = ((r0 + r1) + r2) / 3
+  struct Lane {
+    hipStream_t own = nullptr;         // lanes > 0: their main stream (lane 0 uses the caller's)
+    std::vector<hipStream_t> branch;   // nbs_ - 1 branch streams
+    hipEvent_t ev_ups = nullptr, ev_done = nullptr;
+    std::vector<hipEvent_t> ev_z;      // per MRF branch
+    int nbs = 1;                       // branch streams this forward uses (<= nbs_)
+  };
   void forward_plain(const float* mel, int B, int C, int T, int pad, const float* g, float* wav, hipStream_t s,
-                     Profiler* prof);
+                     Profiler* prof, float* ws, Lane* lane);
+  void ensure_lanes();
+  int64_t lane_bytes(int B, int64_t L) const;
+  int lane_batch(int B, int i) const { return B / n_lanes_ + (i < B % n_lanes_ ? 1 : 0); }
   bool windowed(int64_t L) const;
   int64_t plain_workspace_bytes(int B, int64_t L) const;
   int64_t window_buffer_bytes(int B, int64_t W) const;
@@ -115,21 +131,21 @@ class Hifigan {
   int64_t cond_floats(int B) const;
   int amax_groups() const;
   int stage_group(int i) const;
-  int n_planes() const;  // activation planes of the workspace (Z, O, then X / T per branch)
-  void ensure_branch_streams();
+  int n_planes() const;  // activation planes of a lane's workspace (Z, O, then X / T per branch stream)
 
   TtsHifiganCfg cfg_;
   int device_;
   int hop_ = 1;
   int rb2_geo64_ = 0;         // ResBlock2 at 64 channels: 1 = 192-column tiles (resblock2_geo64)
   bool post_fusion_ = true;  // conv_post inside the last MRF launch (TTS_MI355X_POST_FUSION=0: off)
-  // MRF branches on concurrent streams (TTS_MI355X_MRF_STREAMS=0: one stream): branch j > 0 runs
-  // on bstream_[j - 1], each branch with its own X / T planes; the branches' final (MRF-sum)
-  // launches stay in order j = 0, 1, ... through events, so z = ((r0 + r1) + r2) / 3 as before
-  bool mrf_streams_ = true;
-  std::vector<hipStream_t> bstream_;
-  hipEvent_t ev_ups_ = nullptr;
-  std::vector<hipEvent_t> ev_z_;
+  // defaults (A/B on MI355X, config 2): two sub-batch lanes with one stream each when B >= 2
+  // (51.5 ms per batch), else one lane with a stream per MRF branch (51.8 ms at B = 32; 3 x 2
+  // streams: 52.5 ms)
+  int nbs_ = 1;      // MRF branch streams per lane (workspace planes are sized for it)
+  int n_lanes_ = 2;  // sub-batches
+  bool nbs_env_ = false;
+  std::vector<Lane> lanes_;
+  hipEvent_t ev_start_ = nullptr;
   ConvLayer pre_;
   std::vector<ConvTLayer> ups_;
   std::vector<ResBlock> res_;
