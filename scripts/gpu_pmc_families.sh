@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmcf
 mkdir -p $OUT
-BENCH="bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits"
+BENCH="bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-alt --no-glow --no-e2e --no-xtts --no-vits --no-vits-tts --no-rb2"
 export TTS_FORWARD_NAMES=$OUT/forward_names.json
 timeout -s KILL 120 rocprofv3 --list-avail > $OUT/counters_avail.txt 2>&1 || true
 i=0
