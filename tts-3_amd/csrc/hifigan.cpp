@@ -125,7 +125,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
     // 0.82 -> 0.60 per launch; TTS_MI355X_WINO=0 keeps the direct kernel).  Kernel 3 is supported
     // but measured within 2-4% of the direct kernel (1.05 vs 1.07 ms at c128), not worth the
     // Winograd rounding, so it stays direct.
-    if (std::string(fam) == "mrf_conv" && K >= 7 && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil)) {
+    // TTS_MI355X_WINO_K3=1 (A/B): kernel 3 at >= 256 channels (stage 1's per-conv k3 path; the
+    // 128-channel k3 block stays a whole-block launch) on the Winograd kernel as well
+    const bool wino_k3 = [] {
+      const char* e = std::getenv("TTS_MI355X_WINO_K3");
+      return e && e[0] == '1';
+    }();
+    const bool k_ok = K >= 7 || (K == 3 && Cout >= 256 && wino_k3);
+    if (std::string(fam) == "mrf_conv" && k_ok && wino_enabled() && wino_supported(lmode, Cout, Cin, K, dil)) {
       L.tile = kSplitWinoTile;
       fam = "mrf_wino";
     }
