@@ -634,3 +634,28 @@ def test_concurrent_schedules_bitwise(cuda_device, monkeypatch, mode):
         assert torch.equal(v, base), f"schedule {k} differs from the one-stream forward ({mode})"
     ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
     assert_close_fp32(base, ref, f"concurrent schedules ({mode})", **tol(mode))
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16", "fp32x6"])
+def test_whole_block_k7_k11_matches_pairs(cuda_device, monkeypatch, mode):
+    """Kernel-7 / 11 ResBlock1 as one launch at 32 and 64 channels (resblock3_kernel with K = 7 / 11,
+    TTS_MI355X_RB1_WHOLE_K) against the pair path, over several workgroups per utterance and a
+    ragged tail: both within the mode's gates of the fp64 oracle and of each other; the profiled
+    launch names show the whole-block launches."""
+    sd = synthetic.hifigan_state_dict(seed=43, weight_norm=False)
+    mel = synthetic.mel(2, 47, seed=5)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    outs = []
+    for wk in ("7,11", ""):
+        monkeypatch.setenv("TTS_MI355X_RB1_WHOLE_K", wk)
+        g = HifiganGenerator(**V1, math_mode=mode)
+        g.remove_weight_norm()
+        g.load_state_dict(sd)
+        g = g.to(cuda_device)
+        outs.append(g.inference(mel.to(cuda_device)).cpu())
+        assert_close_fp32(outs[-1], ref, f"{mode} whole k={wk!r}", **tol(mode))
+        names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+        if wk:
+            for nm in ("mrf_block_k7_c32", "mrf_block_k11_c32", "mrf_block_k7_c64", "mrf_block_k11_c64"):
+                assert names.count(nm) == 1, (nm, names)
+    assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)

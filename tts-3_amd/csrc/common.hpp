@@ -128,7 +128,7 @@ struct ResBlock3Args {
   int T;
 };
 bool resblock3_supported(int mode, int C, int K, const int* dil);
-void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s);
+void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, int K, hipStream_t s);
 // A whole ResBlock2 (hifigan_generator.py:150-155: two convs of kernel K, dilations dil[0..1],
 // each x = conv(lrelu(x)) + x) in one kernel; ResBlock3Args with w / bias / w_exp[0..1].
 // geo64 = 1: 192-column tiles at C = 64 (default 128)

@@ -224,8 +224,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
           if (std::string(e) == "all") return 1 << 30;
           return std::atoi(e);
         }();
+        // kernels 7 / 11 as whole blocks (TTS_MI355X_RB1_WHOLE_K lists them, e.g. "7" or "7,11"; A/B)
+        const std::string wk = [] {
+          const char* e = std::getenv("TTS_MI355X_RB1_WHOLE_K");
+          return std::string(e ? e : "");
+        }();
+        const bool k_ok = k == 3 || wk.find(std::to_string(k)) != std::string::npos;
         if (cfg_.resblock_type == 1)
-          rb.fused3 = ch <= policy && resblock3_supported(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
+          rb.fused3 = ch <= policy && k_ok && resblock3_supported(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
         else
           rb.fused2 = ch <= policy && resblock2_preferred(mode, ch, k, cfg_.resblock_dilation_sizes[j]);
       }
@@ -685,7 +691,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 6.0 * L1.Cout * L1.Cin * L1.K);
         const std::string nm = "mrf_block_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
         zorder();
-        run(prof, sj, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, sj); });
+        run(prof, sj, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, L1.K, sj); });
         zdone();
       } else if (cfg_.resblock_type == 1 && rb.fused) {
         // x_{m+1} = convs2[m](lrelu(convs1[m](lrelu(x_m)))) + x_m in one launch per m; the

@@ -461,44 +461,64 @@ void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, h
 
 
 namespace {
-template <class S, int C, int GEO>
+template <class S, int C, int GEO, int K>
 void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
-  using P = Res3Cfg<S, C, GEO>;
+  using P = Res3Cfg<S, C, GEO, K, 6, r3_xoff(K), r3_lead(K)>;
   dim3 grid(ceil_div(a.T, P::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, 3, 6, R3_XOFF, R3_LEAD>), grid, dim3(P::NT), 0, s, a);
+  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, K, 6, r3_xoff(K), r3_lead(K)>), grid, dim3(P::NT), 0, s, a);
 }
 template <class S>
-void launch_res3_s(const ResBlock3Args& a, int B, int C, hipStream_t s) {
+void launch_res3_s(const ResBlock3Args& a, int B, int C, int K, hipStream_t s) {
   // C = 64: 128 columns (2 waves/SIMD, a quarter of the columns are halo; 192 columns at one
   // wave per SIMD measured slower).  C = 128: 128 columns as 8 waves of 32 rows x 64 columns (two
-  // per SIMD; 2 x 2 waves of 64 x 64 measured slower); LDS 8 x 138 rows
-  if (C == 32) launch_res3_t<S, 32, 0>(a, B, s);
+  // per SIMD; 2 x 2 waves of 64 x 64 measured slower); LDS 8 x 138 rows.  Kernels 7 / 11 (32 and
+  // 64 channels): the 256-column tile keeps 184 / 136 columns
+  if (K == 7) {
+    if (C == 32) launch_res3_t<S, 32, 0, 7>(a, B, s);
+    else launch_res3_t<S, 64, 0, 7>(a, B, s);
+    return;
+  }
+  if (K == 11) {
+    if (C == 32) launch_res3_t<S, 32, 0, 11>(a, B, s);
+    else launch_res3_t<S, 64, 0, 11>(a, B, s);
+    return;
+  }
+  if (C == 32) launch_res3_t<S, 32, 0, 3>(a, B, s);
   else if (C == 128) {
-    if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 3>(a, B, s);
+    if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 3, 3>(a, B, s);
     else throw Error(3, "resblock3: 128 channels need a split scheme of at most 80-byte rows");
-  } else launch_res3_t<S, 64, 2>(a, B, s);
+  } else launch_res3_t<S, 64, 2, 3>(a, B, s);
 }
 }  // namespace
 
 bool resblock3_supported(int mode, int C, int K, const int* dil) {
-  // C = 128 stages 8 groups x 138 rows: 88 KB of LDS for f16x3 / 53 KB for bf16 (x6 is not built)
-  if (!is_split_mode(mode) || !(C == 32 || C == 64 || (C == 128 && mode != MATH_FP32_X6)) || K != 3) return false;
-  // the kernel's valid-range walk: kept columns [R3_LEAD, RP_W - R3_LEAD) must stay inside it
-  int lo = -R3_XOFF;
-  for (int m = 0; m < 3; ++m) {
-    if (dil[m] < 1 || dil[m] > R3_XOFF) return false;
-    lo = std::max(lo + dil[m], 0) + 1;
+  // C = 128 stages 8 groups x 138 rows: 88 KB of LDS for f16x3 / 53 KB for bf16 (x6 is not built);
+  // kernels 7 / 11 at 32 / 64 channels (256-column tiles)
+  if (!is_split_mode(mode)) return false;
+  if (K == 3) {
+    if (!(C == 32 || C == 64 || (C == 128 && mode != MATH_FP32_X6))) return false;
+  } else if (K == 7 || K == 11) {
+    if (!(C == 32 || C == 64)) return false;
+  } else {
+    return false;
   }
-  return lo <= R3_LEAD;
+  // the kernel's valid-range walk: kept columns [LEAD, RP_W - LEAD) must stay inside it
+  const int hk = (K - 1) / 2;
+  int lo = -r3_xoff(K);
+  for (int m = 0; m < 3; ++m) {
+    if (dil[m] < 1 || hk * dil[m] > r3_xoff(K)) return false;
+    lo = std::max(lo + hk * dil[m], 0) + hk;
+  }
+  return lo <= r3_lead(K);
 }
 
-void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, hipStream_t s) {
-  TTS_REQUIRE(resblock3_supported(mode, C, 3, a.dil), 3, "resblock3: unsupported configuration");
+void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, int K, hipStream_t s) {
+  TTS_REQUIRE(resblock3_supported(mode, C, K, a.dil), 3, "resblock3: unsupported configuration");
   TTS_REQUIRE(a.zmode >= 1 && a.zmode <= 3 && a.z && a.x && a.x != a.z, 1, "resblock3: bad arguments");
   TTS_REQUIRE((int64_t)C * a.T * 4 < (int64_t(1) << 31), 3, "resblock3: plane exceeds 2 GiB");
-  if (mode == MATH_FP32_F16X3) launch_res3_s<SchemeH3>(a, B, C, s);
-  else if (mode == MATH_BF16) launch_res3_s<SchemeB1>(a, B, C, s);
-  else launch_res3_s<SchemeX6>(a, B, C, s);
+  if (mode == MATH_FP32_F16X3) launch_res3_s<SchemeH3>(a, B, C, K, s);
+  else if (mode == MATH_BF16) launch_res3_s<SchemeB1>(a, B, C, K, s);
+  else launch_res3_s<SchemeX6>(a, B, C, K, s);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

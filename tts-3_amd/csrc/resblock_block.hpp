@@ -32,6 +32,11 @@ namespace tts {
 #endif
 constexpr int R3_XOFF = 5;
 constexpr int R3_LEAD = 12;
+// ResBlock1 of kernel K (round 5: 7 and 11 at 32 / 64 channels): every conv's halo scales by
+// (K - 1) / 2, so X rows hold column + 5 (K - 1) / 2 and the kept columns lose 12 (K - 1) / 2
+// (K 7: 15 / 36, K 11: 25 / 60)
+constexpr int r3_xoff(int K) { return R3_XOFF * ((K - 1) / 2); }
+constexpr int r3_lead(int K) { return R3_LEAD * ((K - 1) / 2); }
 // ResBlock2 kernel K: XO = LEAD = (K - 1) / 2 * the largest dilation it takes (K 3: 4, K 5: 6,
 // K 7 / 11: 3; HiFiGAN-v3 [[1, 2], [2, 6], [3, 12]] up to kernel 5, YourTTS (1, 3) for 3, 7, 11)
 constexpr int rb2_halo(int K) { return K == 3 ? 4 : (K == 5 ? 12 : (K == 7 ? 9 : 15)); }
@@ -61,7 +66,7 @@ __global__ __launch_bounds__((Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>::NT))
 __attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) || GEO == 3 ? 2 : 1)))
 void resblock3_kernel(ResBlock3Args a) {
   using P = Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>;
-  static_assert(NCV == 6 ? K == 3 : NCV == 2, "ResBlock1 (6 convs, kernel 3) or ResBlock2 (2 convs)");
+  static_assert(NCV == 6 || NCV == 2, "ResBlock1 (6 convs) or ResBlock2 (2 convs)");
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC, PR = P::PR, RP_W = P::RP_W;
