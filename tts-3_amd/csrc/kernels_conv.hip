@@ -543,14 +543,29 @@ __global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, yv), ry, inb ? (int)((unsigned)ti * 4u) : (int)OOB_OFF, 0, 0);
 }
 
+// cvec[b][co] = bc[co] + sum_k Wc[co][k] g[b][k] (cond_layer, a 1x1 conv of g).  A block takes
+// outputs co0 .. co0 + 255 of utterance b; the Wc rows pass through LDS 32 columns at a time with
+// coalesced loads (one thread per row read 1 KB-strided rows: 40 us per VITS flow call), then each
+// thread runs its own row's FMA chain in k order, the same operations as one thread per output
 __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const float* Wc, const float* bc,
                                                      float* cvec, int B, int Cc, int C0) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= B * C0) return;
-  const int b = i / C0, co = i - b * C0;
+  __shared__ float wt[256][33];
+  __shared__ float gs[32];
+  const int b = blockIdx.y, co0 = blockIdx.x * 256, t = threadIdx.x;
   float acc = 0.f;
-  for (int k = 0; k < Cc; ++k) acc = fmaf(Wc[(size_t)co * Cc + k], g[(size_t)b * Cc + k], acc);
-  cvec[i] = acc + bc[co];
+  for (int k0 = 0; k0 < Cc; k0 += 32) {
+    const int kn = Cc - k0 < 32 ? Cc - k0 : 32;
+    __syncthreads();  // the previous columns are consumed
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) {
+      const int r = (t >> 5) + 8 * j, k = t & 31;
+      wt[r][k] = (co0 + r < C0 && k < kn) ? Wc[(size_t)(co0 + r) * Cc + k0 + k] : 0.f;
+    }
+    if (t < 32) gs[t] = t < kn ? g[(size_t)b * Cc + k0 + t] : 0.f;
+    __syncthreads();
+    for (int k = 0; k < kn; ++k) acc = fmaf(wt[t][k], gs[k], acc);
+  }
+  if (co0 + t < C0) cvec[(size_t)b * C0 + co0 + t] = acc + bc[co0 + t];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -717,8 +732,7 @@ void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
 
 void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
                      int C0, hipStream_t s) {
-  hipLaunchKernelGGL(cond_vec_kernel, dim3(ceil_div(B * C0, 256)), dim3(256), 0, s, g, Wc, bc, cvec, B,
-                     Cc, C0);
+  hipLaunchKernelGGL(cond_vec_kernel, dim3(ceil_div(C0, 256), B), dim3(256), 0, s, g, Wc, bc, cvec, B, Cc, C0);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

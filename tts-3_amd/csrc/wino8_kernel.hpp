@@ -183,10 +183,36 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
   // job index j = 0..3 -> channel piece (a spread lane maps its jobs 0, 1 onto its pair; 2, 3 are empty)
   auto piece = [&](int j) { return SPREAD && grp != TG ? 2 * jp + j : j; };
-  const int jrow = u >> 2, jq = u & 3;  // the lane's unit: column row, channel quad
+  const int jrow0 = u >> 2, jq0 = u & 3;  // the lane's unit: column row, channel quad
+#ifndef WINO8_REMAT
+#define WINO8_REMAT 0  // A/B: 1 = kernels 3 / 7 recompute the unit as kernel 11 does
+#endif
+#ifndef WINO8_REMAT11
+#define WINO8_REMAT11 1
+#endif
+  // kernel 11: the dense group recomputes its unit from the lane id at every job.  That kernel runs
+  // at the 256-VGPR limit and otherwise spills these lane-derived offsets (36 B of scratch, every
+  // reload a scratch load with a vmcnt wait behind the weight prefetches): k11 c128 -3%, c256 -2%.
+  // Kernel 7 does not spill and runs 2.5% slower with the recomputation
+  // (profiles/ab_r05_wino_remat.txt)
+  constexpr bool remat = K == 11 ? WINO8_REMAT11 : WINO8_REMAT;
+  auto job_unit = [&](int& jrow, int& jq) {
+    if (remat && WINO8_DENSE && grp == TG) {
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      const int uu = wm * 64 + ln;
+      jrow = uu >> 2;
+      jq = uu & 3;
+    } else {
+      jrow = jrow0;
+      jq = jq0;
+    }
+  };
   auto job_load = [&](int rb, int j) {
     if (SPREAD && grp != TG && j >= 2) return;
     if (!uok) return;
+    int jrow, jq;
+    job_unit(jrow, jq);
     if constexpr (D == 1) {
       const f32x4* raw4 =
           reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * (C::RPITCH / 4) + jrow;
@@ -203,6 +229,8 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   auto job_finish = [&](int tb, int j) {
     if (SPREAD && grp != TG && j >= 2) return;
     if (!uok) return;
+    int jrow, jq;
+    job_unit(jrow, jq);
     float v[7], t[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
