@@ -13,4 +13,5 @@ dev = torch.device("cuda", 0)
 for mode in sys.argv[1:] or ["f16x3"]:
     r = bench.glow_bench(dev, mode, steps=30, warmup=5, cpu=False)
     print(json.dumps({"mode": mode, "ms_per_step": round(r["ms_per_step"], 4), "launches": r["launches_per_step"],
-                      "kernel_sum_ms": round(r["kernel_sum_ms"], 3)}))
+                      "kernel_sum_ms": round(r["kernel_sum_ms"], 3),
+                      "top": dict(list(r["breakdown_ms"].items())[:4])}))

@@ -40,6 +40,16 @@ double logdet_fp64(const float* w, int S) {
 }
 
 int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil) {
+  // A/B switches for the flow convs' tile (split modes, plain tiles 0-19): TTS_MI355X_FLOW_TILE_K
+  // for the in_layers (K > 1), TTS_MI355X_FLOW_TILE_1X1 for start / res_skip / end
+  if (is_split_mode(mode)) {
+    const char* e = std::getenv(K > 1 ? "TTS_MI355X_FLOW_TILE_K" : "TTS_MI355X_FLOW_TILE_1X1");
+    if (e && *e) {
+      const int t = std::atoi(e);
+      TTS_REQUIRE(t >= 0 && t < kSplitGateTile, 1, "flow tile override out of range");
+      return t;
+    }
+  }
   return conv_tile_for(mode, Cout, K, Cin, dil, false);
 }
 
@@ -58,6 +68,18 @@ bool flow_wn_fused(int mode, int H) {
   // epilogue's h / skip gathers after the last MFMA cost what the update kernel did
   const char* e = std::getenv("TTS_MI355X_WN_FUSION");
   return (e && e[0] == '1') && is_split_mode(mode) && H % 32 == 0;
+}
+
+bool flow_wn_layer(int mode, int H, int K, int dilation_rate, int L) {
+  const char* e = std::getenv("TTS_MI355X_WN_LAYER");
+  if (e && e[0] == '0') return false;
+  if (flow_wn_fused(mode, H)) return false;  // the opt-in arms keep their own launches
+  int d = 1;
+  for (int l = 0; l < L; ++l) {
+    if (!glow_wn_layer_supported(mode, H, K, d) || flow_gate_fused(mode, H, K, d)) return false;
+    d *= dilation_rate;
+  }
+  return true;
 }
 
 bool flow_amax_prepass() {
@@ -133,6 +155,8 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   glow_validate(cfg_);
   amax_prepass_ = flow_amax_prepass();
   wn_fused_ = flow_wn_fused(cfg_.math_mode, cfg_.hidden_channels);
+  wn_layer_ = flow_wn_layer(cfg_.math_mode, cfg_.hidden_channels, cfg_.kernel_size, cfg_.dilation_rate,
+                            cfg_.num_coupling_layers);
   DeviceGuard g(device_);
   const auto shapes = glow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -327,9 +351,31 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
     conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq, slots(fi, 0), slots(fi, 1));
+    float* hcur = hb;
+    float* hnext = xin;  // the one-launch layers' second h buffer (they have no xin plane)
     for (int l = 0; l < L; ++l) {
       // x_in = in_layers[l](h) + g_l  (wavenet.py:101-107; g_l = cond rows [2Hl, 2H(l+1)))
       const float* gl = cvec ? cvec + (size_t)l * 2 * H : nullptr;
+      if (wn_layer_) {  // wavenet.py:101-115 in one launch
+        const Conv& ci = F.in_layers[l];
+        const Conv& cr = F.res_skip[l];
+        const ConvTile ti = conv_tile(cfg_.math_mode, ci.tile), tr = conv_tile(cfg_.math_mode, cr.tile);
+        GlowWnLayerArgs w{};
+        w.h_in = hcur; w.h_out = hnext; w.skip = skip; w.mask = msq;
+        w.w_in = ci.w; w.b_in = ci.b; w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
+        w.w_rs = cr.w; w.b_rs = cr.b;
+        w.amax_h = slots(fi, 1 + l);
+        w.amax_out = l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1);
+        w.w_exp_in = ci.w_exp; w.w_exp_rs = cr.w_exp;
+        w.steps_in = ci.n_chunks * (ti.CK / 16) * ci.K;
+        w.steps_rs = cr.n_chunks * (tr.CK / 16);
+        w.rs_blocks = ceil_div(cr.Cout, tr.BM) * tr.BM / 32;
+        w.H = H; w.Th = Th; w.K = ci.K; w.dil = ci.dil; w.first = l == 0; w.last = l == L - 1;
+        run(prof, s, "glow_wn_layer", 2.0 * P * H * (2.0 * H * ci.K + cr.Cout), 4.0 * P * H * 4,
+            [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
+        std::swap(hcur, hnext);
+        continue;
+      }
       if (F.in_layers[l].gated) {  // wavenet.py:101 + :108 in one launch, acts straight from the epilogue
         conv("glow_wn_in_gate", F.in_layers[l], hb, 0, acts, nullptr, slots(fi, 1 + l), slots(fi, 1 + L + l), gl);
       } else {

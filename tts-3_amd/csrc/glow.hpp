@@ -40,6 +40,10 @@ int flow_conv_tile(int mode, int Cout, int K, int Cin, int dil);
 // TTS_MI355X_FLOW_GATE=1 at create time (opt-in: measured slower end to end at config 3).
 bool flow_gate_fused(int mode, int H, int K, int dil);
 bool flow_wn_fused(int mode, int H);
+// Whether the WN layers of a flow run as one launch each (launch_glow_wn_layer): split modes, the
+// supported (H, K, dilations), no opt-in gate / update fusion, unless TTS_MI355X_WN_LAYER=0 at
+// create time (layer l's dilation: dilation_rate^l, wavenet.py:68)
+bool flow_wn_layer(int mode, int H, int K, int dilation_rate, int L);
 // f16x3 statistics of each flow's x0 (the start / pre conv input): by default the previous flow's
 // last writer publishes them (the Glow tail kernel, the VITS post conv epilogue) and only the first
 // flow runs a strided max-abs pre-pass; TTS_MI355X_FLOW_AMAX_PREPASS=1 at create time runs the
@@ -54,6 +58,36 @@ void launch_glow_gate(const float* xin, float* acts, int B, int H, int Th, hipSt
 void launch_glow_wn_update(float* h, float* skip, const float* rs, const float* mask, int B, int H,
                            int Th, int first, int last, hipStream_t s, unsigned* amax = nullptr);
 void launch_glow_tail(const GlowTailArgs& a, int B, hipStream_t s);
+
+// One WaveNet layer in one launch (wavenet.py:101-115): in_layer (H -> 2H, kernel K, dilation) +
+// bias + cond -> fused_add_tanh_sigmoid_multiply -> res_skip (1x1) -> the h / skip update, per
+// 32-column tile with the whole hidden width in the workgroup: xin, acts and rs never reach HBM,
+// and 4 launches per layer become 1.  h is double-buffered (h_out != h_in: neighbouring tiles still
+// read h_in's halo).  The fp32 operations are those of the unfused launches in the same order; in
+// f16x3 the acts operand takes the fixed exponent of |acts| < 1 (the unfused res_skip's own
+// per-utterance exponent whenever max |acts| >= 0.5), bf16 / bf16x6 take no scale.
+// TTS_MI355X_WN_LAYER=0 at create time keeps the four launches per layer.
+struct GlowWnLayerArgs {
+  const float* h_in;     // [B][H][Th]
+  float* h_out;          // [B][H][Th] (not the last layer)
+  float* skip;           // [B][H][Th], = rs[H:] (first layer) or += (later ones)
+  const float* mask;     // [B][Th]
+  const float* w_in;     // in_layer, split packing (32-row blocks of steps_in steps)
+  const float* b_in;     // [2H]
+  const float* cvec;     // g_l rows [2H] of item b at cvec + b * cvec_bstride, or nullptr
+  int64_t cvec_bstride;
+  const float* w_rs;     // res_skip (1x1) split packing, rs_rows = 2H (H for the last layer)
+  const float* b_rs;
+  const unsigned* amax_h;  // f16x3: max-abs slots of h_in (its producer's), else nullptr
+  unsigned* amax_out;      // f16x3: slots of h_out (not last) or skip (last), else nullptr
+  int w_exp_in, w_exp_rs;
+  int steps_in, steps_rs;  // packed steps per 32-row block
+  int rs_blocks;           // 32-row blocks allocated in w_rs
+  int H, Th, K, dil, first, last;
+};
+// split modes, H in {128, 192, 256}, K in {3, 5}, (K - 1) * dil <= 16
+bool glow_wn_layer_supported(int mode, int H, int K, int dil);
+void launch_glow_wn_layer(int mode, const GlowWnLayerArgs& a, int B, hipStream_t s);
 // forward direction (reverse=False)
 struct GlowHeadArgs {  // ActNorm -> InvConvNear forward of one flow block, in place
   float* x;            // [B][C2][Th]
@@ -129,6 +163,7 @@ class GlowDecoder {
   size_t ws_bytes_ = 0;
   bool amax_prepass_ = false;
   bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
+  bool wn_layer_ = false;  // every WN layer in one launch (glow_wn_layer_kernel, flow_wn_layer)
 };
 
 }  // namespace tts
