@@ -17,4 +17,7 @@ out["vits"] = {k: round(x["ms_per_step"], 3) for k, x in v["variants"].items()}
 out["xtts"] = round(bench.xtts_decoder_bench(dev, "f16x3")["ms_per_step"], 3)
 e = bench.glow_tts_e2e_bench(dev, {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")})
 out["e2e"] = {k: round(x["ms_per_step"], 3) for k, x in e["variants"].items()}
+if os.environ.get("SIDE_VITS_TTS"):
+    t = bench.vits_tts_bench(dev)
+    out["vits_tts"] = {k: round(x["ms_per_step"], 3) for k, x in t["variants"].items()}
 print(json.dumps(out))

@@ -103,6 +103,7 @@ def test_vits_gate_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
     mask = (torch.arange(257)[None] < torch.tensor([257, 100])[:, None]).float().unsqueeze(1).to(cuda_device)
     g = torch.randn(2, cond, 1, generator=gen).to(cuda_device) if cond else None
     outs = []
+    monkeypatch.setenv("TTS_MI355X_WN_LAYER", "0")  # the per-conv launches (one-launch layers: below)
     for fused in ("1", "0"):
         monkeypatch.setenv("TTS_MI355X_FLOW_GATE", fused)
         f, _ = build(cfg, 31, cuda_device, mode)
@@ -127,6 +128,7 @@ def test_vits_wn_update_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
     pcfg = dict(in_channels=64, out_channels=48, hidden_channels=96, kernel_size=5, dilation_rate=1, num_layers=6,
                 cond_channels=cond)
     outs = []
+    monkeypatch.setenv("TTS_MI355X_WN_LAYER", "0")
     for fused in ("1", "0"):
         monkeypatch.setenv("TTS_MI355X_WN_FUSION", fused)
         f, _ = build(cfg, 31, cuda_device, mode)
@@ -136,6 +138,43 @@ def test_vits_wn_update_fusion_bitwise(cuda_device, mode, cond, monkeypatch):
         outs.append((f(x, mask, g=g, reverse=True), f(x, mask, g=g, reverse=False), pe(spec, lens, g=g, noise=eps)[0]))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("cond", [0, 16])
+def test_vits_wn_layer_matches_unfused(cuda_device, mode, cond, monkeypatch):
+    """One launch per WaveNet layer (kernels_glow_wn.hip) in the coupling flows (both directions) and
+    the posterior encoder's 16-layer WN, against the four launches per layer: bitwise in bf16, the
+    fp32-faithful tolerance in f16x3 / bf16x6 (test_glow_gpu.py explains why)."""
+    cfg = dict(VITS_FLOW, num_flows=2, cond_channels=cond)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(2, cfg["channels"], 257, generator=gen).to(cuda_device)
+    mask = (torch.arange(257)[None] < torch.tensor([257, 100])[:, None]).float().unsqueeze(1).to(cuda_device)
+    g = torch.randn(2, cond, 1, generator=gen).to(cuda_device) if cond else None
+    spec = torch.randn(2, 64, 257, generator=gen).to(cuda_device)
+    eps = torch.randn(2, 48, 257, generator=gen).to(cuda_device)
+    lens = torch.tensor([257, 100]).to(cuda_device)
+    pcfg = dict(in_channels=64, out_channels=48, hidden_channels=192, kernel_size=5, dilation_rate=1, num_layers=16,
+                cond_channels=cond)
+    outs, names = [], []
+    for on in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_LAYER", on)
+        f, _ = build(cfg, 31, cuda_device, mode)
+        pe = PosteriorEncoder(**pcfg, math_mode=mode)
+        pe.load_state_dict(synthetic.vits_posterior_state_dict(**pcfg, seed=7))
+        pe = pe.to(cuda_device)
+        outs.append((f(x, mask, g=g, reverse=True), f(x, mask, g=g, reverse=False), pe(spec, lens, g=g, noise=eps)[0]))
+        names.append([r["name"] for r in f.profile(x, mask, g=g)[1]])
+    L = cfg["num_layers"]
+    assert names[0].count("vits_wn_layer") == 2 * L and "vits_gate" not in names[0]
+    assert names[1].count("vits_gate") == 2 * L and "vits_wn_layer" not in names[1]
+    for what, a, b in zip(("reverse", "forward", "posterior z"), *outs):
+        if mode == "bf16":
+            assert torch.equal(a, b), what
+        else:
+            # posterior z = m + eps * exp(logs) after 16 layers: an absolute gate scaled to its magnitude
+            scale = max(1.0, b.abs().max().item())
+            assert_close_fp32(a.cpu(), b.cpu().double().numpy(), f"vits wn layer {what} {mode}", 1e-5 * scale, 5e-6)
 
 
 @pytest.mark.parametrize("cond", [0, 16])

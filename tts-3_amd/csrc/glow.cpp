@@ -359,18 +359,11 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
       if (wn_layer_) {  // wavenet.py:101-115 in one launch
         const Conv& ci = F.in_layers[l];
         const Conv& cr = F.res_skip[l];
-        const ConvTile ti = conv_tile(cfg_.math_mode, ci.tile), tr = conv_tile(cfg_.math_mode, cr.tile);
-        GlowWnLayerArgs w{};
+        GlowWnLayerArgs w = wn_layer_weights(cfg_.math_mode, ci, cr, H, Th, l, L);
         w.h_in = hcur; w.h_out = hnext; w.skip = skip; w.mask = msq;
-        w.w_in = ci.w; w.b_in = ci.b; w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
-        w.w_rs = cr.w; w.b_rs = cr.b;
+        w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
         w.amax_h = slots(fi, 1 + l);
         w.amax_out = l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1);
-        w.w_exp_in = ci.w_exp; w.w_exp_rs = cr.w_exp;
-        w.steps_in = ci.n_chunks * (ti.CK / 16) * ci.K;
-        w.steps_rs = cr.n_chunks * (tr.CK / 16);
-        w.rs_blocks = ceil_div(cr.Cout, tr.BM) * tr.BM / 32;
-        w.H = H; w.Th = Th; w.K = ci.K; w.dil = ci.dil; w.first = l == 0; w.last = l == L - 1;
         run(prof, s, "glow_wn_layer", 2.0 * P * H * (2.0 * H * ci.K + cr.Cout), 4.0 * P * H * 4,
             [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
         std::swap(hcur, hnext);

@@ -88,6 +88,20 @@ struct GlowWnLayerArgs {
 // split modes, H in {128, 192, 256}, K in {3, 5}, (K - 1) * dil <= 16
 bool glow_wn_layer_supported(int mode, int H, int K, int dil);
 void launch_glow_wn_layer(int mode, const GlowWnLayerArgs& a, int B, hipStream_t s);
+// The weight fields of layer l (l of L) from its in_layer / res_skip convs (any executor's Conv with
+// w, b, w_exp, tile, n_chunks, Cout, K, dil); the caller fills the planes, cond and statistics
+template <class Cv>
+GlowWnLayerArgs wn_layer_weights(int mode, const Cv& ci, const Cv& cr, int H, int Th, int l, int L) {
+  const ConvTile ti = conv_tile(mode, ci.tile), tr = conv_tile(mode, cr.tile);
+  GlowWnLayerArgs w{};
+  w.w_in = ci.w; w.b_in = ci.b; w.w_rs = cr.w; w.b_rs = cr.b;
+  w.w_exp_in = ci.w_exp; w.w_exp_rs = cr.w_exp;
+  w.steps_in = ci.n_chunks * (ti.CK / 16) * ci.K;
+  w.steps_rs = cr.n_chunks * (tr.CK / 16);
+  w.rs_blocks = ceil_div(cr.Cout, tr.BM) * tr.BM / 32;
+  w.H = H; w.Th = Th; w.K = ci.K; w.dil = ci.dil; w.first = l == 0; w.last = l == L - 1;
+  return w;
+}
 // forward direction (reverse=False)
 struct GlowHeadArgs {  // ActNorm -> InvConvNear forward of one flow block, in place
   float* x;            // [B][C2][Th]

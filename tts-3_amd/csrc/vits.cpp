@@ -67,6 +67,8 @@ VitsFlow::VitsFlow(const TtsVitsFlowCfg& cfg, const float* const* hw, int device
   vits_flow_validate(cfg_);
   amax_prepass_ = flow_amax_prepass();
   wn_fused_ = flow_wn_fused(cfg_.math_mode, cfg_.hidden_channels);
+  wn_layer_ = flow_wn_layer(cfg_.math_mode, cfg_.hidden_channels, cfg_.kernel_size, cfg_.dilation_rate,
+                            cfg_.num_layers);
   DeviceGuard g(device_);
   const auto shapes = vits_flow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -276,9 +278,22 @@ void VitsFlow::run_flows(bool rev, const float* x, const float* mask, const floa
     // h = pre(x0) * mask  (networks.py:157)
     conv("vits_pre", Fl.pre, y + Fl.in_off * T, xbs, hb, mask, nullptr, 0, nullptr, 0, false, slots(fi, 0),
          slots(fi, 1));
+    float* hcur = hb;
+    float* hnext = xin;  // the one-launch layers' second h buffer
     for (int l = 0; l < L; ++l) {
       // x_in = in_layers[l](h) (+ g_l)   (wavenet.py:101-107)
       const float* gl = cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr;
+      if (wn_layer_) {  // wavenet.py:101-115 in one launch
+        GlowWnLayerArgs w = wn_layer_weights(cfg_.math_mode, Fl.in_layers[l], Fl.res_skip[l], H, T, l, L);
+        w.h_in = hcur; w.h_out = hnext; w.skip = skip; w.mask = mask;
+        w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
+        w.amax_h = slots(fi, 1 + l);
+        w.amax_out = l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1);
+        run(prof, s, "vits_wn_layer", 2.0 * P * H * (2.0 * H * Fl.in_layers[l].K + Fl.res_skip[l].Cout),
+            4.0 * P * H * 4, [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
+        std::swap(hcur, hnext);
+        continue;
+      }
       if (Fl.in_layers[l].gated) {  // in_layer + g_l + gate (:108) in one launch
         conv("vits_wn_in_gate", Fl.in_layers[l], hb, 0, acts, nullptr, nullptr, 0, gl, (int64_t)2 * H * L, false,
              slots(fi, 1 + l), slots(fi, 1 + L + l));
@@ -367,6 +382,8 @@ void vits_posterior_validate(const TtsVitsPosteriorCfg& c) {
 VitsPosterior::VitsPosterior(const TtsVitsPosteriorCfg& cfg, const float* const* hw, int device)
     : cfg_(cfg), device_(device) {
   vits_posterior_validate(cfg_);
+  wn_layer_ = flow_wn_layer(cfg_.math_mode, cfg_.hidden_channels, cfg_.kernel_size, cfg_.dilation_rate,
+                            cfg_.num_layers);
   DeviceGuard g(device_);
   const auto shapes = vits_posterior_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -501,8 +518,21 @@ void VitsPosterior::forward(const float* x, const float* mask, const float* g, c
     run(prof, s, "vits_post_amax", 0.0, 4.0 * P * C, [&] { launch_amax(x, (int64_t)C * T, B, slots(0), s); });
   // h = pre(x) * mask (networks.py:283)
   conv("vits_post_pre", pre_, x, hb, mask, nullptr, slots(0), slots(1));
+  float* hcur = hb;
+  float* hnext = xin;  // the one-launch layers' second h buffer
   for (int l = 0; l < L; ++l) {  // WN (wavenet.py:94-115)
     const float* gl = cfg_.cond_channels > 0 ? cvec + (size_t)l * 2 * H : nullptr;
+    if (wn_layer_) {  // wavenet.py:101-115 in one launch
+      GlowWnLayerArgs w = wn_layer_weights(cfg_.math_mode, in_layers_[l], res_skip_[l], H, T, l, L);
+      w.h_in = hcur; w.h_out = hnext; w.skip = skip; w.mask = mask;
+      w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
+      w.amax_h = slots(1 + l);
+      w.amax_out = l < L - 1 ? slots(2 + l) : slots(2 * L + 1);
+      run(prof, s, "vits_post_wn_layer", 2.0 * P * H * (2.0 * H * in_layers_[l].K + res_skip_[l].Cout),
+          4.0 * P * H * 4, [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
+      std::swap(hcur, hnext);
+      continue;
+    }
     if (in_layers_[l].gated) {
       conv("vits_post_wn_in_gate", in_layers_[l], hb, acts, nullptr, gl, slots(1 + l), slots(1 + L + l));
     } else {

@@ -55,6 +55,7 @@ class VitsFlow {
   size_t ws_bytes_ = 0;
   bool amax_prepass_ = false;
   bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
+  bool wn_layer_ = false;  // every WN layer in one launch (launch_glow_wn_layer, flow_wn_layer)
 };
 
 std::vector<int64_t> vits_posterior_weight_shapes(const TtsVitsPosteriorCfg& c);
@@ -88,6 +89,7 @@ class VitsPosterior {
   int device_;
   Conv pre_, proj_;
   std::vector<Conv> in_layers_, res_skip_;
+  bool wn_layer_ = false;  // every WN layer in one launch (launch_glow_wn_layer, flow_wn_layer)
   float* cond_w_ = nullptr;
   float* cond_b_ = nullptr;
   float* arena_ = nullptr;
