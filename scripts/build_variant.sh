@@ -8,7 +8,7 @@ V=build_v_$name
 rm -rf $V && mkdir -p $V ../abx && cp build/*.o $V/
 for tu in "$@"; do
   extra=""
-  case $tu in kernels_conv_wino|kernels_resblock|kernels_resblock2_*|kernels_convT_res|kernels_conv_split_h3|kernels_conv_split_b1|kernels_conv_split_x6) extra=-fno-slp-vectorize;; esac
+  case $tu in kernels_conv_wino|kernels_resblock|kernels_resblock2_*|kernels_convT_res|kernels_conv_split_h3|kernels_conv_split_b1|kernels_conv_split_x6|kernels_glow_wn) extra=-fno-slp-vectorize;; esac
   case $tu in kernels_conv*|kernels_resblock*) extra="$extra -Xarch_device -fno-honor-nans";; esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -Icsrc -Wall -Wno-unused-function $extra $defs -c csrc/$tu.hip -o $V/$tu.hip.o &
 done

@@ -1,0 +1,15 @@
+# PMC passes over the Glow decoder side line (scripts/glow_ab.py f16x3), per-dispatch averages of the
+# one-launch WN layer kernel
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/wnpmc
+mkdir -p $OUT
+i=0
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum"; do
+  i=$((i+1))
+  timeout -s KILL 180 rocprofv3 --pmc $grp -d $OUT/p$i -o p$i --output-format csv -- python3 scripts/glow_ab.py f16x3 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 scripts/kernel_pmc_avg.py "glow_wn_layer|glow_end|glow_start" $(ls $OUT/p*/p*_counter_collection.csv)

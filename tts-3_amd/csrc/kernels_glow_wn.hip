@@ -26,7 +26,26 @@ constexpr int WN_COLS = 32;                   // output columns per workgroup
 constexpr int WN_HALO_MAX = 16;               // (K - 1) * dil
 constexpr int WN_XR = WN_COLS + WN_HALO_MAX;  // staged h rows, at most
 constexpr int WN_XP = WN_COLS + 1;            // fp32 pitch of the xin tile rows
-constexpr int WN_PD = 2;                      // A-operand prefetch distance (steps)
+#ifndef WN_PD
+#define WN_PD 2  // A-operand prefetch distance (steps)
+#endif
+// tuning switches (A/B builds): WN_STAGE_BATCH issues every h-window load of a thread before its
+// first LDS store (one HBM latency instead of one per staging round); WN_EARLY_A issues each GEMM's
+// first WN_PD weight steps before the work that precedes it (the staging, the gate); WN_EPI_EARLY
+// loads the update epilogue's h / skip / bias operands before the res_skip GEMM
+#ifndef WN_STAGE_BATCH
+#define WN_STAGE_BATCH 1
+#endif
+#ifndef WN_EARLY_A
+#define WN_EARLY_A 1
+#endif
+#ifndef WN_ABLATE
+#define WN_ABLATE 0  // timing ablations only (wrong results): 1 no MFMAs, 2 no A loads in the loops,
+                     // 4 no gate transcendentals, 8 no h-window loads, 16 no res_skip GEMM
+#endif
+#ifndef WN_EPI_EARLY
+#define WN_EPI_EARLY 0  // measured neutral to slightly slower (profiles/ab_r05_wn_tune.txt)
+#endif
 constexpr int WN_ACTS_EXP = -14;              // f16x3 exponent of acts: |acts| < 1 -> [0, 2^14)
 
 template <class S, int TMW>
@@ -46,18 +65,27 @@ struct WnCfg {
 // from LDS by bsrc(g, k, dst); the same product order per accumulator as conv1d_split_kernel.
 // Every block is computed (phase 2 of the last layer points its surplus blocks at a valid one and
 // drops them in the epilogue): no branches around the MFMAs
-template <class S, int TMW, int KS, class BSrc>
-__device__ __forceinline__ void wn_gemm(f32x16 (&acc)[TMW], const rsrc_t (&ra)[TMW], int ngroups, unsigned avoff,
-                                        BSrc bsrc) {
-  constexpr int NP = S::NP;
-  f32x4 ar[WN_PD + 1][TMW][NP], bcur[NP], bnext[NP];
+// The first WN_PD steps' A fragments (the GEMM's prologue; wn_gemm expects them in ar[0 .. PD-1])
+template <class S, int TMW>
+__device__ __forceinline__ void wn_prefetch(f32x4 (&ar)[WN_PD + 1][TMW][S::NP], const rsrc_t (&ra)[TMW], unsigned avoff) {
 #pragma unroll
   for (int p = 0; p < WN_PD; ++p)
 #pragma unroll
     for (int m = 0; m < TMW; ++m)
 #pragma unroll
-      for (int q = 0; q < NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * NP + q) * 1024u);
+      for (int q = 0; q < S::NP; ++q) ar[p][m][q] = bload4(ra[m], avoff, (unsigned)(p * S::NP + q) * 1024u);
+}
+
+// fully unrolled (NGR groups x KS taps): the prefetch ring and the B double buffer are renamed
+// registers, with no moves, loop counters or branches between the MFMAs
+template <class S, int TMW, int KS, int NGR, class BSrc>
+__device__ __forceinline__ void wn_gemm(f32x16 (&acc)[TMW], f32x4 (&ar)[WN_PD + 1][TMW][S::NP], const rsrc_t (&ra)[TMW],
+                                        unsigned avoff, BSrc bsrc) {
+  constexpr int NP = S::NP;
+  constexpr int ngroups = NGR;
+  f32x4 bcur[NP], bnext[NP];
   bsrc(0, 0, bcur);
+#pragma unroll
   for (int g = 0; g < ngroups; ++g) {
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -65,7 +93,8 @@ __device__ __forceinline__ void wn_gemm(f32x16 (&acc)[TMW], const rsrc_t (&ra)[T
 #pragma unroll
       for (int m = 0; m < TMW; ++m)
 #pragma unroll
-        for (int q = 0; q < NP; ++q) ar[WN_PD][m][q] = bload4(ra[m], avoff, (unsigned)((s + WN_PD) * NP + q) * 1024u);
+        for (int q = 0; q < NP; ++q)
+          ar[WN_PD][m][q] = (WN_ABLATE & 2) ? ar[0][m][q] : bload4(ra[m], avoff, (unsigned)((s + WN_PD) * NP + q) * 1024u);
       const bool nx = (k + 1 < KS) || (g + 1 < ngroups);
       if (nx) bsrc((k + 1 < KS) ? g : g + 1, (k + 1 < KS) ? k + 1 : 0, bnext);
       __builtin_amdgcn_sched_barrier(0);
@@ -73,7 +102,7 @@ __device__ __forceinline__ void wn_gemm(f32x16 (&acc)[TMW], const rsrc_t (&ra)[T
       for (int e = 0; e < S::NPROD; ++e)
 #pragma unroll
         for (int m = 0; m < TMW; ++m)
-          acc[m] = S::mfma(ar[0][m][S::PA[e]], bcur[S::PB[e]], acc[m]);
+          if (!(WN_ABLATE & 1)) acc[m] = S::mfma(ar[0][m][S::PA[e]], bcur[S::PB[e]], acc[m]);
 #pragma unroll
       for (int p = 0; p < WN_PD; ++p)
 #pragma unroll
@@ -120,36 +149,67 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   // ---- stage the h window: unit u = (group g, channel quad q, row r), 4 channels of one frame
   const int ex = H3 ? amax_exp(a.amax_h, b) : 0;
   const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;  // exact power of two
-  {
-    const rsrc_t rh = make_rsrc(a.h_in + item, plane);
-    const int units = NG * 4 * XR;
-    for (int u = tid; u < units; u += 256) {
-      const int r = u % XR;
-      const int gq = u / XR;
-      const int q = gq & 3, g = gq >> 2;
-      const int ts = t0 - pad + r;
-      const unsigned off = (ts >= 0 && ts < Th) ? (unsigned)(16 * g + 4 * q) * rowb + (unsigned)ts * 4u : OOB_OFF;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = bload(rh, off + (unsigned)j * rowb, 0u);
-        if (H3) v[j] *= xscale;
-      }
-      split_store4<S>(hwin + (g * XR + r) * S::ROWB + 8 * quad_pos(q), v[0], v[1], v[2], v[3]);
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 1: in_layer, wave w on 32-row blocks w + 4 m (4 TMW = 2H / 32 blocks)
+  // phase 1's weights: wave w on 32-row blocks w + 4 m (4 TMW = 2H / 32 blocks)
   f32x16 acc[TMW];
   bool on[TMW];
   rsrc_t ra[TMW];
+  f32x4 ar[WN_PD + 1][TMW][NP];
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     acc[m] = f32x16{};
     ra[m] = make_rsrc(a.w_in + (size_t)(w + 4 * m) * a.steps_in * (NP * 256), 0xFFFFFFFFu);
   }
-  wn_gemm<S, TMW, K>(acc, ra, NG, avoff, [&](int g, int k, f32x4* dst) {
+  if (WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
+  {
+    const rsrc_t rh = make_rsrc(a.h_in + item, plane);
+    const int units = NG * 4 * XR;
+    auto unit_off = [&](int u, int& lds) -> unsigned {
+      const int r = u % XR;
+      const int gq = u / XR;
+      const int q = gq & 3, g = gq >> 2;
+      const int ts = t0 - pad + r;
+      lds = (g * XR + r) * S::ROWB + 8 * quad_pos(q);
+      return (u < units && ts >= 0 && ts < Th) ? (unsigned)(16 * g + 4 * q) * rowb + (unsigned)ts * 4u : OOB_OFF;
+    };
+    if (WN_STAGE_BATCH) {
+      constexpr int UPT = (NG * 4 * WN_XR + 255) / 256;
+      float v[UPT][4];
+      int lds[UPT];
+#pragma unroll
+      for (int i = 0; i < UPT; ++i) {
+        const unsigned off = unit_off(tid + 256 * i, lds[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] = (WN_ABLATE & 8) ? 0.f : bload(rh, off + (unsigned)j * rowb, 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < UPT; ++i) {
+        if (tid + 256 * i < units) {
+          if (H3) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[i][j] *= xscale;
+          }
+          split_store4<S>(hwin + lds[i], v[i][0], v[i][1], v[i][2], v[i][3]);
+        }
+      }
+    } else {
+      for (int u = tid; u < units; u += 256) {
+        int lds;
+        const unsigned off = unit_off(u, lds);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = bload(rh, off + (unsigned)j * rowb, 0u);
+          if (H3) v[j] *= xscale;
+        }
+        split_store4<S>(hwin + lds, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 1: in_layer
+  if (!WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
+  wn_gemm<S, TMW, K, NG>(acc, ar, ra, avoff, [&](int g, int k, f32x4* dst) {
     const unsigned char* p = hwin + (g * XR + l32 + k * d) * S::ROWB + 16 * half;
 #pragma unroll
     for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
@@ -174,6 +234,16 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
       }
     }
   }
+  // phase 2's weights (res_skip, 2H rows, the last layer H): wave w on blocks w + 4 m
+  const int nmb = (a.last ? H : 2 * H) / 32;
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    const int mb = w + 4 * m;
+    acc[m] = f32x16{};
+    on[m] = mb < nmb;
+    ra[m] = make_rsrc(a.w_rs + (size_t)(mb < a.rs_blocks ? mb : w) * a.steps_rs * (NP * 256), 0xFFFFFFFFu);
+  }
+  if (WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
   __syncthreads();
 
   // ---- gate: acts = tanh(xin[c]) * sigmoid(xin[H + c]) (glow_gate_kernel), 4 channels per unit
@@ -188,8 +258,8 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
         const int c = 4 * cq + j;
         const float x = xin[c * WN_XP + col];
         const float gg = xin[(H + c) * WN_XP + col];
-        const float sg = 1.f / (1.f + expf(-gg));
-        av[j] = tanhf(x) * sg;
+        const float sg = (WN_ABLATE & 4) ? gg : 1.f / (1.f + expf(-gg));
+        av[j] = ((WN_ABLATE & 4) ? x : tanhf(x)) * sg;
         if (H3) av[j] *= ascale;
       }
       split_store4<S>(acts + ((cq >> 2) * WN_COLS + col) * S::ROWB + 8 * quad_pos(cq & 3), av[0], av[1], av[2], av[3]);
@@ -197,16 +267,38 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   }
   __syncthreads();
 
-  // ---- phase 2: res_skip (2H rows, the last layer H), wave w on blocks w + 4 m
-  const int nmb = (a.last ? H : 2 * H) / 32;
+  // ---- update epilogue operands (glow_wn_update_kernel's on v = rs): h_in / skip / bias per block
+  const int t = t0 + l32;
+  const bool tok = t < Th;
+  const rsrc_t rbias = make_rsrc(a.b_rs, (unsigned)nmb * 128u);
+  const rsrc_t rmask = make_rsrc(a.mask + (size_t)b * Th, rowb);
+  const rsrc_t rhi = make_rsrc(a.h_in + item, plane);
+  const rsrc_t rho = make_rsrc(a.last ? a.h_in + item : a.h_out + item, a.last ? 0u : plane);
+  const rsrc_t rsk = make_rsrc(a.skip + item, plane);
+  const bool first = a.first != 0, last = a.last != 0;
+  float ov[TMW][16], bv[TMW][16];
+  float mv = 0.f;
+  auto epi_loads = [&]() {
+    mv = bload(rmask, tok ? (unsigned)t * 4u : OOB_OFF, 0u);
 #pragma unroll
-  for (int m = 0; m < TMW; ++m) {
-    const int mb = w + 4 * m;
-    acc[m] = f32x16{};
-    on[m] = mb < nmb;
-    ra[m] = make_rsrc(a.w_rs + (size_t)(mb < a.rs_blocks ? mb : w) * a.steps_rs * (NP * 256), 0xFFFFFFFFu);
-  }
-  wn_gemm<S, TMW, 1>(acc, ra, NG, avoff, [&](int g, int, f32x4* dst) {
+    for (int m = 0; m < TMW; ++m) {
+      const int mb = w + 4 * m;
+      const bool hrow = !last && mb < H / 32;  // wave-uniform: a 32-row block is one side
+      const int prow0 = (hrow || last ? 32 * mb : 32 * mb - H) + 4 * half;
+      const unsigned voff = (tok && on[m]) ? ((unsigned)prow0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned ro = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
+        ov[m][r] = hrow ? bload(rhi, ro, 0u) : (first ? 0.f : bload(rsk, ro, 0u));
+        bv[m][r] = bload(rbias, (unsigned)(32 * mb + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
+      }
+    }
+  };
+  if (WN_EPI_EARLY) epi_loads();
+
+  // ---- phase 2: res_skip
+  if (!WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
+  if (!(WN_ABLATE & 16)) wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
     const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
 #pragma unroll
     for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
@@ -218,45 +310,30 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   }
 
   // ---- update epilogue (glow_wn_update_kernel's operations on v = rs)
-  const int t = t0 + l32;
-  const bool tok = t < Th;
-  const rsrc_t rbias = make_rsrc(a.b_rs, (unsigned)nmb * 128u);
-  const rsrc_t rmask = make_rsrc(a.mask + (size_t)b * Th, rowb);
-  const rsrc_t rhi = make_rsrc(a.h_in + item, plane);
-  const rsrc_t rho = make_rsrc(a.last ? a.h_in + item : a.h_out + item, a.last ? 0u : plane);
-  const rsrc_t rsk = make_rsrc(a.skip + item, plane);
-  const float mv = bload(rmask, tok ? (unsigned)t * 4u : OOB_OFF, 0u);
-  const bool first = a.first != 0, last = a.last != 0;
+  if (!WN_EPI_EARLY) epi_loads();
   float vmax = 0.f;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     const int mb = w + 4 * m;
     if (!on[m]) continue;
-    const bool hrow = !last && mb < H / 32;  // wave-uniform: a 32-row block is one side
+    const bool hrow = !last && mb < H / 32;
     const int prow0 = (hrow || last ? 32 * mb : 32 * mb - H) + 4 * half;
     const unsigned voff = tok ? ((unsigned)prow0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
-    float ov[16], bv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const unsigned ro = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-      ov[r] = hrow ? bload(rhi, ro, 0u) : (first ? 0.f : bload(rsk, ro, 0u));
-      bv[r] = bload(rbias, (unsigned)(32 * mb + (r & 3) + 8 * (r >> 2) + 4 * half) * 4u, 0u);
-    }
     float vm = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const unsigned ro = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-      const float v = acc[m][r] + bv[r];
+      const float v = acc[m][r] + bv[m][r];
       if (hrow) {
-        const float o = (ov[r] + v) * mv;
+        const float o = (ov[m][r] + v) * mv;
         vm = fmaxf(vm, fabsf(o));
         bstore(rho, o, ro, 0u);
       } else if (last) {
-        const float o = (first ? v : ov[r] + v) * mv;
+        const float o = (first ? v : ov[m][r] + v) * mv;
         vm = fmaxf(vm, fabsf(o));
         bstore(rsk, o, ro, 0u);
       } else {
-        bstore(rsk, first ? v : ov[r] + v, ro, 0u);
+        bstore(rsk, first ? v : ov[m][r] + v, ro, 0u);
       }
     }
     if (tok) vmax = fmaxf(vmax, vm);
