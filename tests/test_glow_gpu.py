@@ -218,6 +218,9 @@ def test_glow_wn_layer_matches_unfused(cuda_device, mode, reverse, cname, monkey
         names.append([r["name"] for r in d.profile(x, m, g=g)[1]])
     L, NF = cfg["num_coupling_layers"], cfg["num_flow_blocks"]
     assert names[0].count("glow_wn_layer") == NF * L and "glow_gate" not in names[0]
+    # the coupling's end conv rides in the last layer's launch when C2 is whole 32-row blocks
+    C2 = cfg["in_channels"] * cfg["num_squeeze"]
+    assert names[0].count("glow_end") == (0 if C2 % 32 == 0 and C2 <= 2 * cfg["hidden_channels"] else NF)
     assert names[1].count("glow_gate") == NF * L and "glow_wn_layer" not in names[1]
     if mode != "bf16":
         assert_close_fp32(outs[0][0].cpu(), outs[1][0].cpu().double().numpy(), f"wn layer {cname} {mode}",
@@ -229,6 +232,31 @@ def test_glow_wn_layer_matches_unfused(cuda_device, mode, reverse, cname, monkey
         assert torch.equal(outs[0][0], outs[1][0])
         if not reverse:
             assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+def test_glow_wn_end_fusion(cuda_device, mode, monkeypatch):
+    """The end conv inside the last WN layer's launch (TTS_MI355X_WN_END) against its own launch:
+    bitwise in bf16 (same operations and order), the fp32-faithful tolerance otherwise (f16x3: the
+    tile's max-abs exponent instead of the utterance's); both directions, logdet included."""
+    cfg = WN_LAYER_CFGS["ljspeech"]
+    gen = torch.Generator().manual_seed(37)
+    x = torch.randn(3, 80, 301, generator=gen).to(cuda_device)
+    m = (torch.arange(301)[None] < torch.tensor([301, 150, 9])[:, None]).float().unsqueeze(1).to(cuda_device)
+    outs = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_END", on)
+        d = build(cfg, 43, cuda_device, mode)
+        outs[on] = (d(x, m, reverse=True)[0], d(x, m, reverse=False))
+        names = [r["name"] for r in d.profile(x, m)[1]]
+        assert names.count("glow_end") == (0 if on == "1" else cfg["num_flow_blocks"])
+    (r1, (f1, l1)), (r0, (f0, l0)) = outs["1"], outs["0"]
+    if mode == "bf16":
+        assert torch.equal(r1, r0) and torch.equal(f1, f0) and torch.equal(l1, l0)
+    else:
+        assert_close_fp32(r1.cpu(), r0.cpu().double().numpy(), f"wn end {mode}", GLOW_MAX_ABS, GLOW_REL_RMS)
+        assert_close_fp32(f1.cpu(), f0.cpu().double().numpy(), f"wn end fwd {mode}", GLOW_MAX_ABS, GLOW_REL_RMS)
+        assert (l1 - l0).abs().max().item() <= 1e-5 * max(1.0, l0.abs().max().item())
 
 
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])

@@ -157,6 +157,11 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
   wn_fused_ = flow_wn_fused(cfg_.math_mode, cfg_.hidden_channels);
   wn_layer_ = flow_wn_layer(cfg_.math_mode, cfg_.hidden_channels, cfg_.kernel_size, cfg_.dilation_rate,
                             cfg_.num_coupling_layers);
+  {
+    const char* e = std::getenv("TTS_MI355X_WN_END");
+    const int C2 = cfg_.in_channels * cfg_.num_squeeze;
+    wn_end_ = wn_layer_ && !(e && e[0] == '0') && C2 % 32 == 0 && C2 <= 2 * cfg_.hidden_channels;
+  }
   DeviceGuard g(device_);
   const auto shapes = glow_weight_shapes(cfg_);
   for (size_t i = 0; i < shapes.size(); ++i)
@@ -364,6 +369,14 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
         w.cvec = gl; w.cvec_bstride = (int64_t)2 * H * L;
         w.amax_h = slots(fi, 1 + l);
         w.amax_out = l < L - 1 ? slots(fi, 2 + l) : slots(fi, 2 * L + 1);
+        if (wn_end_ && l == L - 1) {  // glow.py:214 in the same launch
+          const ConvTile te = conv_tile(cfg_.math_mode, F.end.tile);
+          w.w_end = F.end.w; w.b_end = F.end.b; w.end_out = out; w.end_rows = F.end.Cout;
+          w.end_steps = F.end.n_chunks * (te.CK / 16);
+          w.end_blocks = ceil_div(F.end.Cout, te.BM) * te.BM / 32;
+          w.w_exp_end = F.end.w_exp;
+          w.amax_out = nullptr;  // skip is not written: nothing reads its statistics
+        }
         run(prof, s, "glow_wn_layer", 2.0 * P * H * (2.0 * H * ci.K + cr.Cout), 4.0 * P * H * 4,
             [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
         std::swap(hcur, hnext);
@@ -393,7 +406,8 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
         });  // :110-115
       }
     }
-    conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));  // glow.py:214
+    if (!(wn_layer_ && wn_end_))
+      conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));  // glow.py:214
   };
 
   if (rev) {

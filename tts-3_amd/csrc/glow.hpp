@@ -84,6 +84,13 @@ struct GlowWnLayerArgs {
   int steps_in, steps_rs;  // packed steps per 32-row block
   int rs_blocks;           // 32-row blocks allocated in w_rs
   int H, Th, K, dil, first, last;
+  // last layer only, optional (w_end != nullptr): the 1x1 conv that consumes skip (the Glow
+  // coupling's `end`, glow.py:214) in the same launch: end_out = w_end * skip + b_end, end_rows
+  // rows; skip itself is then not written.  Its f16x3 operand scale is the tile's max-abs exponent.
+  const float* w_end;
+  const float* b_end;
+  float* end_out;        // [B][end_rows][Th]
+  int end_rows, end_steps, end_blocks, w_exp_end;
 };
 // split modes, H in {128, 192, 256}, K in {3, 5}, (K - 1) * dil <= 16
 bool glow_wn_layer_supported(int mode, int H, int K, int dil);
@@ -178,6 +185,7 @@ class GlowDecoder {
   bool amax_prepass_ = false;
   bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
   bool wn_layer_ = false;  // every WN layer in one launch (glow_wn_layer_kernel, flow_wn_layer)
+  bool wn_end_ = false;    // ... and the coupling's end conv inside the last one (TTS_MI355X_WN_END)
 };
 
 }  // namespace tts

@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   constexpr int H = C::H;
   constexpr int NG = C::NG;
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
+  __shared__ float red[4];  // the end conv's per-tile max-abs
   unsigned char* hwin = smem;                   // stage / phase 1: the h window (split pieces)
   float* xin = reinterpret_cast<float*>(smem);  // after phase 1: xin tile [2H][WN_XP] fp32
   unsigned char* acts = smem + C::U1;           // phase 2's B operand (split pieces)
@@ -311,6 +312,8 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 
   // ---- update epilogue (glow_wn_update_kernel's operations on v = rs)
   if (!WN_EPI_EARLY) epi_loads();
+  const bool fuse_end = last && a.w_end != nullptr;  // uniform
+  float so[TMW][16];  // fuse_end: this wave's final skip values (the end conv's B operand)
   float vmax = 0.f;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
@@ -331,14 +334,78 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
       } else if (last) {
         const float o = (first ? v : ov[m][r] + v) * mv;
         vm = fmaxf(vm, fabsf(o));
-        bstore(rsk, o, ro, 0u);
+        so[m][r] = o;
+        if (!fuse_end) bstore(rsk, o, ro, 0u);
       } else {
         bstore(rsk, first ? v : ov[m][r] + v, ro, 0u);
       }
     }
     if (tok) vmax = fmaxf(vmax, vm);
   }
-  if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+  if (!fuse_end) {
+    if (H3 && a.amax_out) publish_amax(a.amax_out, b, vmax);
+    return;
+  }
+
+  // ---- phase 3 (last layer): end_out = w_end * skip + b_end (conv1d_split_kernel's operations;
+  // f16x3: the operand exponent of this tile's max |skip| instead of the utterance's)
+  int et = 0;
+  if (H3) {
+    const float m = wave_max(vmax);
+    if (lane == 0) red[w] = m;
+  }
+  __syncthreads();  // the max, and every wave is done reading acts
+  if (H3) {
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f && m < INFINITY) {
+      int E;
+      (void)frexpf(m, &E);
+      et = E - 14;
+    }
+  }
+  const float sin_ = H3 ? ldexpf(1.f, -et) : 1.f;
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    if (!on[m]) continue;
+    const int mb = w + 4 * m;  // skip rows 32 mb .. + 31: channel groups 2 mb, 2 mb + 1
+#pragma unroll
+    for (int gs = 0; gs < 2; ++gs)
+      store_xt8<S>(acts + ((2 * mb + gs) * WN_COLS + l32) * S::ROWB + 16 * half, so[m], 8 * gs, sin_);
+  }
+  const int nmb3 = a.end_rows / 32;
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    const int mb = w + 4 * m;
+    acc[m] = f32x16{};
+    on[m] = mb < nmb3;
+    ra[m] = make_rsrc(a.w_end + (size_t)(mb < a.end_blocks ? mb : w) * a.end_steps * (NP * 256), 0xFFFFFFFFu);
+  }
+  wn_prefetch<S, TMW>(ar, ra, avoff);
+  __syncthreads();
+  wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
+    const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
+  });
+  if constexpr (H3) {
+    const float sc = ldexpf(1.f, et + a.w_exp_end);
+#pragma unroll
+    for (int m = 0; m < TMW; ++m) acc[m] *= sc;
+  }
+  const rsrc_t rbe = make_rsrc(a.b_end, (unsigned)a.end_rows * 4u);
+  const rsrc_t reo = make_rsrc(a.end_out + (size_t)b * a.end_rows * Th, (unsigned)a.end_rows * rowb);
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    if (!on[m]) continue;
+    const int row0 = 32 * (w + 4 * m) + 4 * half;
+    const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2);
+      const float bvv = bload(rbe, (unsigned)(row0 + rr) * 4u, 0u);
+      bstore(reo, (acc[m][r] + bvv) * 1.f, voff + (unsigned)rr * rowb, 0u);
+    }
+  }
 }
 
 template <class S, int TMW>
@@ -374,6 +441,10 @@ void launch_glow_wn_layer(int mode, const GlowWnLayerArgs& a, int B, hipStream_t
               1, "glow_wn_layer: weight packing does not match");
   TTS_REQUIRE(B >= 1 && a.Th >= 1 && (int64_t)a.H * a.Th * 4 < (int64_t(1) << 31), 3,
               "glow_wn_layer: a batch item's channel plane exceeds 2 GiB");
+  TTS_REQUIRE(!a.w_end || (a.last && a.b_end && a.end_out && a.end_rows % 32 == 0 && a.end_rows >= 32 &&
+                           a.end_rows <= 2 * a.H && a.end_steps == a.H / 16 && a.end_blocks >= a.end_rows / 32 &&
+                           (int64_t)a.end_rows * a.Th * 4 < (int64_t(1) << 31)),
+              1, "glow_wn_layer: bad fused end conv arguments");
   if (mode == MATH_FP32_F16X3) launch_wn_h<SchemeH3>(a, B, s);
   else if (mode == MATH_BF16) launch_wn_h<SchemeB1>(a, B, s);
   else launch_wn_h<SchemeX6>(a, B, s);
