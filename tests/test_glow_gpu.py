@@ -259,6 +259,35 @@ def test_glow_wn_end_fusion(cuda_device, mode, monkeypatch):
         assert (l1 - l0).abs().max().item() <= 1e-5 * max(1.0, l0.abs().max().item())
 
 
+@pytest.mark.parametrize("mode", ["fp32x6", "f16x3", "bf16"])
+@pytest.mark.parametrize("cname", ["ljspeech", "spk_c16"])
+def test_glow_wn_tail_fusion(cuda_device, mode, cname, monkeypatch):
+    """Reverse flows: the inverse tail (coupling, InvConvNear, ActNorm) and the next flow's start conv
+    inside the last WN layer's launch (TTS_MI355X_WN_TAIL) against their own launches: bitwise in
+    bf16; the fp32-faithful tolerance otherwise (f16x3: the start operand's tile exponent); the last
+    flow keeps its tail launch and the first its start launch."""
+    cfg = WN_LAYER_CFGS[cname]
+    NF = cfg["num_flow_blocks"]
+    gen = torch.Generator().manual_seed(41)
+    x = torch.randn(3, 80, 301, generator=gen).to(cuda_device)
+    m = (torch.arange(301)[None] < torch.tensor([301, 150, 9])[:, None]).float().unsqueeze(1).to(cuda_device)
+    c_in = cfg.get("c_in_channels", 0)
+    g = torch.randn(3, c_in, 1, generator=gen).to(cuda_device) if c_in else None
+    outs = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_TAIL", on)
+        d = build(cfg, 47, cuda_device, mode)
+        outs[on] = d(x, m, g=g, reverse=True)[0]
+        names = [r["name"] for r in d.profile(x, m, g=g)[1]]
+        assert names.count("glow_tail") == (1 if on == "1" else NF)
+        assert names.count("glow_start") == (1 if on == "1" else NF)
+    if mode == "bf16":
+        assert torch.equal(outs["1"], outs["0"])
+    else:
+        assert_close_fp32(outs["1"].cpu(), outs["0"].cpu().double().numpy(), f"wn tail {cname} {mode}",
+                          GLOW_MAX_ABS, GLOW_REL_RMS)
+
+
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])
 def test_glow_wn_layer_other_shapes_vs_oracle(cuda_device, mode):
     """The one-launch WN layer at H 128 (kernel 3, dilations 1, 2, 4, 8) against the fp64 oracle."""

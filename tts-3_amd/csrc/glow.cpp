@@ -161,6 +161,8 @@ GlowDecoder::GlowDecoder(const TtsGlowDecoderCfg& cfg, const float* const* hw, i
     const char* e = std::getenv("TTS_MI355X_WN_END");
     const int C2 = cfg_.in_channels * cfg_.num_squeeze;
     wn_end_ = wn_layer_ && !(e && e[0] == '0') && C2 % 32 == 0 && C2 <= 2 * cfg_.hidden_channels;
+    const char* et = std::getenv("TTS_MI355X_WN_TAIL");
+    wn_tail_ = wn_end_ && !(et && et[0] == '0') && cfg_.num_splits == 4 && 3 * C2 <= 4 * cfg_.hidden_channels;
   }
   DeviceGuard g(device_);
   const auto shapes = glow_weight_shapes(cfg_);
@@ -347,7 +349,11 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
   // x0 statistics: the max-abs slots of flow fi's start-conv input come from the previous
   // elementwise kernel (the tail / head / coupling kernels) except for the first reverse flow, or
   // from a strided pre-pass for every flow (TTS_MI355X_FLOW_AMAX_PREPASS=1)
-  auto coupling_net = [&](const Flow& F, int fi) {
+  // reverse flows with the one-launch layers: the last layer of flow fi may also run the flow's
+  // inverse tail and the next flow's start conv (wn_tail_), leaving the next flow's h in pending_h
+  float* pending_h = nullptr;
+  auto coupling_net = [&](const Flow& F, int fi, const Flow* next_start = nullptr) -> bool {
+    bool tail_fused = false;
     if (cvec)  // g = cond_layer(g) (wavenet.py:98-99); every flow has its own cond_layer
       run(prof, s, "glow_cond", 2.0 * B * 2 * H * L * cfg_.c_in_channels, 4.0 * B * 2 * H * L,
           [&] { launch_cond_vec(g, F.cond_w, F.cond_b, cvec, B, cfg_.c_in_channels, 2 * H * L, s); });
@@ -355,9 +361,15 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
       run(prof, s, "glow_amax_x0", 0.0, 2.0 * P * C2,
           [&] { launch_amax(xs, (int64_t)(C2 / 2) * Th, B, slots(fi, 0), s, (int64_t)C2 * Th); });
     // h = start(x_0) * mask  (glow.py:212; x_0 = first C2/2 channels of xs)
-    conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq, slots(fi, 0), slots(fi, 1));
     float* hcur = hb;
     float* hnext = xin;  // the one-launch layers' second h buffer (they have no xin plane)
+    if (pending_h) {  // computed by the previous flow's last layer
+      hcur = pending_h;
+      hnext = pending_h == hb ? xin : hb;
+      pending_h = nullptr;
+    } else {
+      conv("glow_start", F.start, xs, (int64_t)C2 * Th, hb, msq, slots(fi, 0), slots(fi, 1));
+    }
     for (int l = 0; l < L; ++l) {
       // x_in = in_layers[l](h) + g_l  (wavenet.py:101-107; g_l = cond rows [2Hl, 2H(l+1)))
       const float* gl = cvec ? cvec + (size_t)l * 2 * H : nullptr;
@@ -376,6 +388,18 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
           w.end_blocks = ceil_div(F.end.Cout, te.BM) * te.BM / 32;
           w.w_exp_end = F.end.w_exp;
           w.amax_out = nullptr;  // skip is not written: nothing reads its statistics
+          if (next_start) {  // glow.py:222-224 -> :102-137 -> normalization.py:96-98, then the next :212
+            const Conv& cs = next_start->start;
+            const ConvTile ts = conv_tile(cfg_.math_mode, cs.tile);
+            w.tail_x = xs; w.winv = F.winv; w.logs = F.logs; w.abias = F.bias;
+            w.sigmoid_scale = cfg_.sigmoid_scale;
+            w.w_start = cs.w; w.b_start = cs.b; w.h_next = hnext; w.amax_hnext = slots(fi + 1, 1);
+            w.start_steps = cs.n_chunks * (ts.CK / 16);
+            w.start_blocks = ceil_div(cs.Cout, ts.BM) * ts.BM / 32;
+            w.w_exp_start = cs.w_exp;
+            pending_h = hnext;
+            tail_fused = true;
+          }
         }
         run(prof, s, "glow_wn_layer", 2.0 * P * H * (2.0 * H * ci.K + cr.Cout), 4.0 * P * H * 4,
             [&] { launch_glow_wn_layer(cfg_.math_mode, w, B, s); });
@@ -408,6 +432,7 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
     }
     if (!(wn_layer_ && wn_end_))
       conv("glow_end", F.end, skip, 0, out, nullptr, slots(fi, 2 * L + 1));  // glow.py:214
+    return tail_fused;
   };
 
   if (rev) {
@@ -415,7 +440,7 @@ void GlowDecoder::run_flows(bool rev, const float* x, const float* mask, const f
     for (int f = NF - 1; f >= 0; --f) {
       const Flow& F = flows_[f];
       const int fi = NF - 1 - f;
-      coupling_net(F, fi);
+      if (coupling_net(F, fi, (wn_tail_ && f > 0) ? &flows_[f - 1] : nullptr)) continue;
       GlowTailArgs ta{};
       ta.x = xs; ta.out = out; ta.mask = msq; ta.winv = F.winv; ta.logs = F.logs; ta.bias = F.bias;
       ta.C2 = C2; ta.Th = Th; ta.S = cfg_.num_splits; ta.sigmoid_scale = cfg_.sigmoid_scale;

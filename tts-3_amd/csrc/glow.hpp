@@ -91,6 +91,20 @@ struct GlowWnLayerArgs {
   const float* b_end;
   float* end_out;        // [B][end_rows][Th]
   int end_rows, end_steps, end_blocks, w_exp_end;
+  // reverse direction, with the end conv, optional (tail_x != nullptr): the flow's inverse tail
+  // (glow_tail_kernel: coupling, InvConvNear, ActNorm; num_splits 4) on the tile's end output, x
+  // updated in place, then the next flow's start conv into h_next (its f16x3 operand exponent:
+  // the tile's max |x0|); end_out, the tail launch and the next start launch are not needed
+  float* tail_x;           // [B][C2 = end_rows][Th]
+  const float* winv;       // [4][4]
+  const float* logs;       // [C2] ActNorm of this flow
+  const float* abias;      // [C2]
+  int sigmoid_scale;
+  const float* w_start;    // next flow's start conv (C2/2 -> H), split packing
+  const float* b_start;
+  float* h_next;           // [B][H][Th], != h_in
+  unsigned* amax_hnext;    // f16x3 slots of h_next, else nullptr
+  int start_steps, start_blocks, w_exp_start;
 };
 // split modes, H in {128, 192, 256}, K in {3, 5}, (K - 1) * dil <= 16
 bool glow_wn_layer_supported(int mode, int H, int K, int dil);
@@ -186,6 +200,7 @@ class GlowDecoder {
   bool wn_fused_ = false;  // res_skip conv + WN update in one launch (flow_wn_fused)
   bool wn_layer_ = false;  // every WN layer in one launch (glow_wn_layer_kernel, flow_wn_layer)
   bool wn_end_ = false;    // ... and the coupling's end conv inside the last one (TTS_MI355X_WN_END)
+  bool wn_tail_ = false;   // ... and, reverse, the tail + the next flow's start conv (TTS_MI355X_WN_TAIL)
 };
 
 }  // namespace tts

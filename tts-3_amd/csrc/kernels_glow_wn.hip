@@ -117,6 +117,31 @@ __device__ __forceinline__ void wn_gemm(f32x16 (&acc)[TMW], f32x4 (&ar)[WN_PD + 
   }
 }
 
+// wn_gemm with a runtime group count (the fused start conv: C2/2 input channels), 1x1 only
+template <class S, int TMW, class BSrc>
+__device__ __forceinline__ void wn_gemm_rt(f32x16 (&acc)[TMW], f32x4 (&ar)[WN_PD + 1][TMW][S::NP], const rsrc_t (&ra)[TMW],
+                                           int ngroups, unsigned avoff, BSrc bsrc) {
+  constexpr int NP = S::NP;
+  f32x4 bcur[NP];
+  for (int g = 0; g < ngroups; ++g) {
+    bsrc(g, 0, bcur);
+#pragma unroll
+    for (int m = 0; m < TMW; ++m)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ar[WN_PD][m][q] = bload4(ra[m], avoff, (unsigned)((g + WN_PD) * NP + q) * 1024u);
+#pragma unroll
+    for (int e = 0; e < S::NPROD; ++e)
+#pragma unroll
+      for (int m = 0; m < TMW; ++m) acc[m] = S::mfma(ar[0][m][S::PA[e]], bcur[S::PB[e]], acc[m]);
+#pragma unroll
+    for (int p = 0; p < WN_PD; ++p)
+#pragma unroll
+      for (int m = 0; m < TMW; ++m)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ar[p][m][q] = ar[p + 1][m][q];
+  }
+}
+
 template <class S, int K, int TMW>
 __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args) {
   using C = WnCfg<S, TMW>;
@@ -393,19 +418,158 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
     for (int m = 0; m < TMW; ++m) acc[m] *= sc;
   }
   const rsrc_t rbe = make_rsrc(a.b_end, (unsigned)a.end_rows * 4u);
-  const rsrc_t reo = make_rsrc(a.end_out + (size_t)b * a.end_rows * Th, (unsigned)a.end_rows * rowb);
+  if (a.tail_x == nullptr) {
+    const rsrc_t reo = make_rsrc(a.end_out + (size_t)b * a.end_rows * Th, (unsigned)a.end_rows * rowb);
+#pragma unroll
+    for (int m = 0; m < TMW; ++m) {
+      if (!on[m]) continue;
+      const int row0 = 32 * (w + 4 * m) + 4 * half;
+      const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2);
+        const float bvv = bload(rbe, (unsigned)(row0 + rr) * 4u, 0u);
+        bstore(reo, (acc[m][r] + bvv) * 1.f, voff + (unsigned)rr * rowb, 0u);
+      }
+    }
+    return;
+  }
+
+  // ---- reverse flows: this flow's inverse tail on the tile's end output (glow_tail_kernel's
+  // operations; num_splits 4), then the next flow's start conv (conv1d_split_kernel's operations,
+  // f16x3 operand exponent of the tile's max |x0|)
+  const int C2 = a.end_rows, hf = C2 / 2;
+  float* eo = xin;                  // [C2][WN_XP] end output (the xin tile is free since the gate)
+  float* x0t = xin + C2 * WN_XP;    // [C2/2][WN_XP] the updated x0 half
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    if (!on[m]) continue;
+    const int row0 = 32 * (w + 4 * m) + 4 * half;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2);
+      const float bvv = bload(rbe, (unsigned)(row0 + rr) * 4u, 0u);
+      eo[(row0 + rr) * WN_XP + l32] = (acc[m][r] + bvv) * 1.f;
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int SP = 4;
+    float Wm[SP][SP];
+#pragma unroll
+    for (int o = 0; o < SP; ++o)
+#pragma unroll
+      for (int g = 0; g < SP; ++g) Wm[o][g] = a.winv[o * SP + g];
+    const int G = C2 / SP;
+    float vx = 0.f;
+    for (int u = tid; u < G * WN_COLS; u += 256) {
+      const int col = u & (WN_COLS - 1);
+      const int i = u / WN_COLS;
+      const int tc = t0 + col;
+      const bool ok = tc < Th;
+      const float m = ok ? a.mask[(size_t)b * Th + tc] : 0.f;
+      float z[SP];
+      int chs[SP];
+#pragma unroll
+      for (int g = 0; g < SP; ++g) {
+        const int aa = g / (SP / 2), j = g % (SP / 2);
+        const int ch = aa * hf + i * (SP / 2) + j;
+        chs[g] = ch;
+        const float xv = ok ? a.tail_x[((size_t)b * C2 + ch) * Th + tc] : 0.f;
+        if (ch < hf) {
+          z[g] = xv;  // z_0 = x_0
+        } else {
+          const float tt = eo[(ch - hf) * WN_XP + col];
+          float sv = eo[ch * WN_XP + col];
+          if (a.sigmoid_scale) sv = logf(1e-6f + 1.f / (1.f + expf(-(sv + 2.f))));
+          z[g] = (xv - tt) * expf(-sv) * m;  // z_1 = (x_1 - t) * exp(-s) * mask
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < SP; ++o) {
+        float v = 0.f;
+#pragma unroll
+        for (int g = 0; g < SP; ++g) v = fmaf(Wm[o][g], z[g], v);
+        v *= m;                                                  // InvConvNear: * x_mask
+        const int ch = chs[o];
+        v = (v - a.abias[ch]) * expf(-a.logs[ch]) * m;           // ActNorm reverse
+        if (ok) a.tail_x[((size_t)b * C2 + ch) * Th + tc] = v;
+        if (ch < hf) {
+          x0t[ch * WN_XP + col] = v;
+          vx = fmaxf(vx, fabsf(v));
+        }
+      }
+    }
+    if (H3) {
+      const float mm = wave_max(vx);
+      if (lane == 0) red[w] = mm;
+    }
+  }
+  __syncthreads();
+  int e2 = 0;
+  if (H3) {
+    const float mm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (mm > 0.f && mm < INFINITY) {
+      int E;
+      (void)frexpf(mm, &E);
+      e2 = E - 14;
+    }
+  }
+  {
+    const float s2 = H3 ? ldexpf(1.f, -e2) : 1.f;
+    for (int u = tid; u < (hf / 4) * WN_COLS; u += 256) {
+      const int col = u & (WN_COLS - 1);
+      const int cq = u / WN_COLS;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = x0t[(4 * cq + j) * WN_XP + col];
+        if (H3) v[j] *= s2;
+      }
+      split_store4<S>(acts + ((cq >> 2) * WN_COLS + col) * S::ROWB + 8 * quad_pos(cq & 3), v[0], v[1], v[2], v[3]);
+    }
+  }
+  const int nmbs = H / 32;
+#pragma unroll
+  for (int m = 0; m < TMW; ++m) {
+    const int mb = w + 4 * m;
+    acc[m] = f32x16{};
+    on[m] = mb < nmbs;
+    ra[m] = make_rsrc(a.w_start + (size_t)(mb < a.start_blocks ? mb : w) * a.start_steps * (NP * 256), 0xFFFFFFFFu);
+  }
+  wn_prefetch<S, TMW>(ar, ra, avoff);
+  __syncthreads();
+  wn_gemm_rt<S, TMW>(acc, ar, ra, hf / 16, avoff, [&](int g, int, f32x4* dst) {
+    const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
+  });
+  if constexpr (H3) {
+    const float sc = ldexpf(1.f, e2 + a.w_exp_start);
+#pragma unroll
+    for (int m = 0; m < TMW; ++m) acc[m] *= sc;
+  }
+  // h_next = (start(x0) + bias) * mask (the start conv's epilogue, glow.py:212)
+  const rsrc_t rbs = make_rsrc(a.b_start, (unsigned)H * 4u);
+  const rsrc_t rhn = make_rsrc(a.h_next + item, plane);
+  float hmax = 0.f;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     if (!on[m]) continue;
     const int row0 = 32 * (w + 4 * m) + 4 * half;
     const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
+    float vm = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = (r & 3) + 8 * (r >> 2);
-      const float bvv = bload(rbe, (unsigned)(row0 + rr) * 4u, 0u);
-      bstore(reo, (acc[m][r] + bvv) * 1.f, voff + (unsigned)rr * rowb, 0u);
+      const float bsv = bload(rbs, (unsigned)(row0 + rr) * 4u, 0u);
+      const float hv = (acc[m][r] + bsv) * mv;
+      vm = fmaxf(vm, fabsf(hv));
+      bstore(rhn, hv, voff + (unsigned)rr * rowb, 0u);
     }
+    if (tok) hmax = fmaxf(hmax, vm);
   }
+  if (H3 && a.amax_hnext) publish_amax(a.amax_hnext, b, hmax);
 }
 
 template <class S, int TMW>
@@ -445,6 +609,10 @@ void launch_glow_wn_layer(int mode, const GlowWnLayerArgs& a, int B, hipStream_t
                            a.end_rows <= 2 * a.H && a.end_steps == a.H / 16 && a.end_blocks >= a.end_rows / 32 &&
                            (int64_t)a.end_rows * a.Th * 4 < (int64_t(1) << 31)),
               1, "glow_wn_layer: bad fused end conv arguments");
+  TTS_REQUIRE(!a.tail_x || (a.w_end && a.winv && a.logs && a.abias && a.w_start && a.b_start && a.h_next &&
+                            a.h_next != a.h_in && a.end_rows % 32 == 0 && 3 * a.end_rows <= 4 * a.H &&
+                            a.start_steps * 16 >= a.end_rows / 2 && a.start_blocks >= a.H / 32),
+              1, "glow_wn_layer: bad fused tail / start arguments");
   if (mode == MATH_FP32_F16X3) launch_wn_h<SchemeH3>(a, B, s);
   else if (mode == MATH_BF16) launch_wn_h<SchemeB1>(a, B, s);
   else launch_wn_h<SchemeX6>(a, B, s);
