@@ -176,6 +176,12 @@ def family_roofline(rows, mode: str):
             "profiled_forward_ms": step_ms}
 
 
+def progress(msg: str):
+    """One line per long phase on stderr (the JSON line stays alone on stdout): a run that goes quiet
+    for minutes, e.g. during the CPU baseline, reads as hung to a watchdog."""
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(mel, n_utts: int, pad: int = 5):
     """Time the CPU oracle on the first ``n_utts`` utterances of the bench's own mel batch (rank 0,
     N=1): one warm-up on one utterance, then the median of 3 runs (same inputs as the
@@ -195,11 +201,13 @@ def cpu_baseline(mel, n_utts: int, pad: int = 5):
     B, _, T = x.shape
     runs = []
     with torch.no_grad():
+        progress(f"cpu baseline: warm-up, then 3 runs on [{B},80,{T}] ({threads} threads)")
         hifigan_ref.hifigan_forward(sd, x[:1], pad=pad, dtype=torch.float32, **cfg)  # warm-up
-        for _ in range(3):
+        for i in range(3):
             t0 = time.perf_counter()
             hifigan_ref.hifigan_forward(sd, x, pad=pad, dtype=torch.float32, **cfg)
             runs.append(time.perf_counter() - t0)
+            progress(f"cpu baseline run {i + 1}/3: {runs[-1]:.1f} s")
     el = statistics.median(runs)
     samples = B * 256 * (T + 2 * pad)
     return {
@@ -918,18 +926,26 @@ def main():
 
     cpu = None
     acc = None
+    if rank == 0:
+        progress(f"timed steps done: {ms_per_step:.2f} ms/step")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         acc = accuracy_check(gens, dev)
         cpu = cpu_baseline(mel, a.cpu_utts, pad)
 
     side = rank == 0 and world == 1
+    if side:
+        progress("side lines")
     glow = glow_bench(dev, a.math_mode, cpu=not a.no_cpu_baseline) if side and not a.no_glow else None
     e2e = (glow_tts_e2e_bench(dev, {"fp32_faithful": ("f16x3", "f16x3"), "bf16": ("bf16", "bf16")})
            if side and not a.no_e2e else None)
+    if side:
+        progress("side lines: glow decoder and Glow-TTS e2e done")
     xtts = xtts_decoder_bench(dev, a.math_mode) if side and not a.no_xtts else None
     vits = vits_bench(dev) if side and not a.no_vits else None
     vits_tts = vits_tts_bench(dev) if side and not a.no_vits_tts else None
     rb2 = rb2_bench(dev) if side and not a.no_rb2 else None
+    if side:
+        progress("side lines done")
 
     if rank == 0:
         rec.update({
