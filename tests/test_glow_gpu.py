@@ -289,6 +289,35 @@ def test_glow_wn_tail_fusion(cuda_device, mode, cname, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["f16x3", "bf16"])
+def test_glow_wn_tail_sigmoid_scale(cuda_device, mode, monkeypatch):
+    """sigmoid_scale=True (glow.py:222-223: s = log(1e-6 + sigmoid(s + 2))) through the fused tail:
+    bitwise in bf16 against the tail launch, and against the fp64 oracle."""
+    cfg = WN_LAYER_CFGS["ljspeech"]
+    sd = synthetic.glow_decoder_state_dict(**cfg, seed=53)
+    gen = torch.Generator().manual_seed(54)
+    x = torch.randn(2, 80, 203, generator=gen)
+    m = (torch.arange(203)[None] < torch.tensor([203, 77])[:, None]).float().unsqueeze(1)
+    outs = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_WN_TAIL", on)
+        d = Decoder(cfg["in_channels"], cfg["hidden_channels"], cfg["kernel_size"], cfg["dilation_rate"],
+                    cfg["num_flow_blocks"], cfg["num_coupling_layers"], dropout_p=0.05,
+                    num_splits=cfg["num_splits"], num_squeeze=cfg["num_squeeze"], sigmoid_scale=True,
+                    math_mode=mode)
+        d.load_state_dict(sd)
+        d.eval()
+        d.store_inverse()
+        d = d.to(cuda_device)
+        outs[on] = d(x.to(cuda_device), m.to(cuda_device), reverse=True)[0]
+    ref = glow_ref.glow_decoder_reverse(sd, x, m, sigmoid_scale=True, **cfg)
+    if mode == "bf16":
+        assert torch.equal(outs["1"], outs["0"])
+        assert_close_fp32(outs["1"].cpu(), ref, "wn tail sigmoid_scale (bf16)", BF16_MAX_ABS, BF16_REL_RMS)
+    else:
+        assert_close_fp32(outs["1"].cpu(), ref, "wn tail sigmoid_scale (f16x3)", GLOW_MAX_ABS, GLOW_REL_RMS)
+
+
+@pytest.mark.parametrize("mode", ["f16x3", "bf16"])
 def test_glow_wn_layer_other_shapes_vs_oracle(cuda_device, mode):
     """The one-launch WN layer at H 128 (kernel 3, dilations 1, 2, 4, 8) against the fp64 oracle."""
     cfg = WN_LAYER_CFGS["h128_k3_dil2"]
