@@ -543,29 +543,37 @@ __global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, yv), ry, inb ? (int)((unsigned)ti * 4u) : (int)OOB_OFF, 0, 0);
 }
 
-// cvec[b][co] = bc[co] + sum_k Wc[co][k] g[b][k] (cond_layer, a 1x1 conv of g).  A block takes
-// outputs co0 .. co0 + 255 of utterance b; the Wc rows pass through LDS 32 columns at a time with
-// coalesced loads (one thread per row read 1 KB-strided rows: 40 us per VITS flow call), then each
-// thread runs its own row's FMA chain in k order, the same operations as one thread per output
+// cvec[b][co] = bc[co] + sum_k Wc[co][k] * g[b][k] (the cond_layer GEMVs, hifigan_generator.py:228,
+// wavenet.py:98-99): one wave per output row, its lanes across k (coalesced row reads, the row
+// held in registers for every batch item), a butterfly sum per item.  A tile-through-LDS form
+// (32 dependent load rounds per 32 columns) took 150 us per call at 1536 x 256.
 __global__ __launch_bounds__(256) void cond_vec_kernel(const float* g, const float* Wc, const float* bc,
                                                      float* cvec, int B, int Cc, int C0) {
-  __shared__ float wt[256][33];
-  __shared__ float gs[32];
-  const int b = blockIdx.y, co0 = blockIdx.x * 256, t = threadIdx.x;
-  float acc = 0.f;
-  for (int k0 = 0; k0 < Cc; k0 += 32) {
-    const int kn = Cc - k0 < 32 ? Cc - k0 : 32;
-    __syncthreads();  // the previous columns are consumed
-#pragma unroll 8
-    for (int j = 0; j < 32; ++j) {
-      const int r = (t >> 5) + 8 * j, k = t & 31;
-      wt[r][k] = (co0 + r < C0 && k < kn) ? Wc[(size_t)(co0 + r) * Cc + k0 + k] : 0.f;
-    }
-    if (t < 32) gs[t] = t < kn ? g[(size_t)b * Cc + k0 + t] : 0.f;
-    __syncthreads();
-    for (int k = 0; k < kn; ++k) acc = fmaf(wt[t][k], gs[k], acc);
+  const int lane = threadIdx.x & 63;
+  const int co = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (co >= C0) return;  // wave-uniform
+  const float* w = Wc + (size_t)co * Cc;
+  constexpr int KR = 8;  // up to 512 input channels in registers, the rest streamed
+  float wr[KR];
+#pragma unroll
+  for (int i = 0; i < KR; ++i) {
+    const int k = lane + 64 * i;
+    wr[i] = k < Cc ? w[k] : 0.f;
   }
-  if (co0 + t < C0) cvec[(size_t)b * C0 + co0 + t] = acc + bc[co0 + t];
+  const float bias = bc[co];
+  for (int b = 0; b < B; ++b) {
+    const float* gb = g + (size_t)b * Cc;
+    float p = 0.f;
+#pragma unroll
+    for (int i = 0; i < KR; ++i) {
+      const int k = lane + 64 * i;
+      if (k < Cc) p = fmaf(wr[i], gb[k], p);
+    }
+    for (int k = 64 * KR + lane; k < Cc; k += 64) p = fmaf(w[k], gb[k], p);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if (lane == 0) cvec[(size_t)b * C0 + co] = p + bias;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -732,7 +740,7 @@ void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
 
 void launch_cond_vec(const float* g, const float* Wc, const float* bc, float* cvec, int B, int Cc,
                      int C0, hipStream_t s) {
-  hipLaunchKernelGGL(cond_vec_kernel, dim3(ceil_div(C0, 256), B), dim3(256), 0, s, g, Wc, bc, cvec, B, Cc, C0);
+  hipLaunchKernelGGL(cond_vec_kernel, dim3(ceil_div(C0, 4)), dim3(256), 0, s, g, Wc, bc, cvec, B, Cc, C0);
   TTS_HIP_CHECK(hipGetLastError());
 }
 
