@@ -146,7 +146,14 @@ int tts_hifigan_reserve(void* handle, int B, int T, int pad);
 /* wav[B][out][hop*(T+2*pad)] = G(replicate_pad(mel[B][C][T], pad)).  pad = 0 is
  * HifiganGenerator.forward, pad = inference_padding is .inference (hifigan_generator.py:281).
  * d_g ([B][cond_channels], may be NULL when cond_channels == 0) is the global conditioning
- * vector (the reference's g[B][cond][1], :250-251). */
+ * vector (the reference's g[B][cond][1], :250-251).
+ * Streams: the call is ordered on hip_stream; internally it forks onto the handle's own lane /
+ * branch streams and joins back before returning.  Those streams, their events and the handle's
+ * workspace are per handle, so one handle must be driven from one caller stream at a time (a
+ * second stream must wait for the first call's completion); use one handle per concurrent stream.
+ * Non-finite mel values are outside the contract: the kernels build without NaN semantics, so a
+ * NaN or inf input yields an unspecified waveform for that utterance (the other utterances of the
+ * batch are unaffected: every statistic is per utterance). */
 int tts_hifigan_forward(void* handle, const float* d_mel, int B, int C, int T, int pad,
                         const float* d_g, float* d_wav, void* hip_stream);
 
@@ -438,38 +445,41 @@ typedef struct TtsVitsTextEncoderCfg {
   int num_heads;           /* 2 */
   int num_layers;          /* 6 */
   int kernel_size;         /* 3 (FFN) */
-  int language_emb_dim;    /* must be 0 (multilingual concat not implemented) */
+  int language_emb_dim;    /* 0, or L > 0 (YourTTS): the transformer runs at H + L channels (since ABI 115) */
   int math_mode;           /* TTS_MATH_FP32, _X6 or TTS_MATH_BF16 */
 } TtsVitsTextEncoderCfg;
 
-/* Host weight order: emb.weight [n_vocab][H]; per layer l: encoder.attn_layers.l.conv_q/k/v/o
- * (weight [H][H][1], bias [H]), emb_rel_k [1][9][dk], emb_rel_v [1][9][dk], encoder.norm_layers_1.l
- * gamma [H], beta [H], encoder.ffn_layers.l.conv_1 (weight [ffn][H][k], bias), conv_2 (weight
- * [H][ffn][k], bias), encoder.norm_layers_2.l gamma, beta; proj.weight [2 out][H][1], proj.bias [2 out]. */
+/* Host weight order, with E = H + language_emb_dim (networks.py:63-64): emb.weight [n_vocab][H]; per
+ * layer l: encoder.attn_layers.l.conv_q/k/v/o (weight [E][E][1], bias [E]), emb_rel_k [1][9][dk],
+ * emb_rel_v [1][9][dk] (dk = E / num_heads), encoder.norm_layers_1.l gamma [E], beta [E],
+ * encoder.ffn_layers.l.conv_1 (weight [ffn][E][k], bias), conv_2 (weight [E][ffn][k], bias),
+ * encoder.norm_layers_2.l gamma, beta; proj.weight [2 out][E][1], proj.bias [2 out]. */
 int tts_vits_text_encoder_num_weights(const TtsVitsTextEncoderCfg* cfg);
 int64_t tts_vits_text_encoder_weight_numel(const TtsVitsTextEncoderCfg* cfg, int index);
 int tts_vits_text_encoder_create(const TtsVitsTextEncoderCfg* cfg, const float* const* host_weights, int device,
                                  void** handle);
 int tts_vits_text_encoder_destroy(void* handle);
-/* (x, m, logs, x_mask) = TextEncoder.forward(tokens, lengths) (networks.py:83-100): tokens [B][T] int64,
- * lengths [B] int64; x [B][H][T], m and logs [B][out][T], x_mask [B][1][T].  T <= 3072. */
-int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
-                                  float* d_x, float* d_m, float* d_logs, float* d_x_mask, void* hip_stream);
-int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
-                                           int T, float* d_x, float* d_m, float* d_logs, float* d_x_mask,
-                                           void* hip_stream, TtsLaunchRecord* records, int max_records,
-                                           int* n_records);
+/* (x, m, logs, x_mask) = TextEncoder.forward(tokens, lengths, lang_emb) (networks.py:83-100): tokens
+ * [B][T] int64, lengths [B] int64, lang_emb [B][language_emb_dim] (NULL when language_emb_dim = 0;
+ * the reference's [B][L][1]); x [B][E][T], m and logs [B][out][T], x_mask [B][1][T].  T <= 3072. */
+int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                  const float* d_lang_emb, int B, int T, float* d_x, float* d_m, float* d_logs,
+                                  float* d_x_mask, void* hip_stream);
+int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                           const float* d_lang_emb, int B, int T, float* d_x, float* d_m,
+                                           float* d_logs, float* d_x_mask, void* hip_stream,
+                                           TtsLaunchRecord* records, int max_records, int* n_records);
 
 /* Mirrors StochasticDurationPredictor.__init__ (TTS/tts/layers/vits/stochastic_duration_predictor.py:
  * 185-227; VITS: in = hidden_channels, hidden 192, kernel 3, 4 flows, cond = embedded_speaker_dim when
  * condition_dp_on_speaker, vits.py:684-692).  ConvFlows use 10 bins, tail bound 5 (:96-104). */
 typedef struct TtsVitsSdpCfg {
-  int in_channels;      /* 192 */
-  int hidden_channels;  /* 192 */
+  int in_channels;      /* 192 (+ language_emb_dim: the text encoder's x width, :191-192) */
+  int hidden_channels;  /* 192 (<= 512) */
   int kernel_size;      /* 3 */
   int num_flows;        /* 4 */
   int cond_channels;    /* 0 = no cond layer */
-  int language_emb_dim; /* must be 0 */
+  int language_emb_dim; /* 0 = no cond_lang layer (since ABI 115) */
   int math_mode;        /* TTS_MATH_FP32, _X6 or TTS_MATH_BF16 (its 1x1 convs) */
 } TtsVitsSdpCfg;
 
@@ -481,19 +491,53 @@ typedef struct TtsVitsSdpCfg {
  *   flows.0.translation [2][1], flows.0.log_scale [2][1]
  *   for f = 1 .. num_flows: flows.f.pre.weight [H][1][1], bias [H]; DDS(flows.f.convs);
  *                           flows.f.proj.weight [29][H][1], bias [29]
- *   if cond_channels: cond.weight [H][cond][1], cond.bias [H] */
+ *   if cond_channels: cond.weight [H][cond][1], cond.bias [H]
+ *   if language_emb_dim: cond_lang.weight [H][L][1], cond_lang.bias [H] */
 int tts_vits_sdp_num_weights(const TtsVitsSdpCfg* cfg);
 int64_t tts_vits_sdp_weight_numel(const TtsVitsSdpCfg* cfg, int index);
 int tts_vits_sdp_create(const TtsVitsSdpCfg* cfg, const float* const* host_weights, int device, void** handle);
 int tts_vits_sdp_destroy(void* handle);
-/* logw [B][1][T] = StochasticDurationPredictor.forward(x, x_mask, g=g, reverse=True, noise_scale)
- * (:242-282): x [B][in][T], x_mask [B][1][T], g [B][cond_channels] or NULL, noise [B][2][T] the
- * standard normal draw of :277 (torch.randn(B, 2, T); NULL = zeros). */
-int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g, const float* d_noise,
-                         float noise_scale, int B, int T, float* d_logw, void* hip_stream);
+/* logw [B][1][T] = StochasticDurationPredictor.forward(x, x_mask, g=g, lang_emb=lang, reverse=True,
+ * noise_scale) (:242-282): x [B][in][T], x_mask [B][1][T], g [B][cond_channels] or NULL, lang
+ * [B][language_emb_dim] or NULL (x = pre(x) + cond(g) + cond_lang(lang), :249-254), noise [B][2][T]
+ * the standard normal draw of :277 (torch.randn(B, 2, T); NULL = zeros). */
+int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                         const float* d_lang_emb, const float* d_noise, float noise_scale, int B, int T,
+                         float* d_logw, void* hip_stream);
 int tts_vits_sdp_reverse_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
-                                  const float* d_noise, float noise_scale, int B, int T, float* d_logw,
-                                  void* hip_stream, TtsLaunchRecord* records, int max_records, int* n_records);
+                                  const float* d_lang_emb, const float* d_noise, float noise_scale, int B, int T,
+                                  float* d_logw, void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                  int* n_records);
+
+/* Mirrors the deterministic DurationPredictor VITS builds with use_sdp=False (vits.py:694-702:
+ * TTS/tts/layers/glow_tts/duration_predictor.py:6-44 with in = hidden_channels, filter 256, kernel 3,
+ * cond = embedded_speaker_dim, language_emb_dim), since ABI 115. */
+typedef struct TtsVitsDpCfg {
+  int in_channels;      /* hidden_channels (192); the module adds language_emb_dim itself (:28-29) */
+  int hidden_channels;  /* filter channels, 256 */
+  int kernel_size;      /* 3 (odd, <= 11) */
+  int cond_channels;    /* 0 = no cond layer */
+  int language_emb_dim; /* 0 = no cond_lang layer */
+  int math_mode;        /* TTS_MATH_FP32, _X6 or TTS_MATH_BF16 */
+} TtsVitsDpCfg;
+
+/* Host weight order (state_dict order), I = in_channels + language_emb_dim, F = hidden_channels:
+ *   conv_1.weight [F][I][k], conv_1.bias [F]; norm_1.gamma [F], norm_1.beta [F];
+ *   conv_2.weight [F][F][k], conv_2.bias [F]; norm_2.gamma [F], norm_2.beta [F];
+ *   proj.weight [1][F][1], proj.bias [1];
+ *   if cond_channels: cond.weight [I][cond][1], cond.bias [I];
+ *   if language_emb_dim: cond_lang.weight [I][L][1], cond_lang.bias [I] */
+int tts_vits_dp_num_weights(const TtsVitsDpCfg* cfg);
+int64_t tts_vits_dp_weight_numel(const TtsVitsDpCfg* cfg, int index);
+int tts_vits_dp_create(const TtsVitsDpCfg* cfg, const float* const* host_weights, int device, void** handle);
+int tts_vits_dp_destroy(void* handle);
+/* logw [B][1][T] = DurationPredictor.forward(x, x_mask, g, lang_emb) (duration_predictor.py:49-68):
+ * x [B][I][T], x_mask [B][1][T], g [B][cond_channels] or NULL, lang [B][language_emb_dim] or NULL. */
+int tts_vits_dp_forward(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                        const float* d_lang_emb, int B, int T, float* d_logw, void* hip_stream);
+int tts_vits_dp_forward_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                                 const float* d_lang_emb, int B, int T, float* d_logw, void* hip_stream,
+                                 TtsLaunchRecord* records, int max_records, int* n_records);
 
 /* vits.py:1145-1148: w_ceil [B][1][T_x] = ceil(exp(logw) * x_mask * length_scale); y_lengths [B]
  * (int64) = max(sum(w_ceil), 1).  The caller reads y_lengths back for T_y = max(y_lengths). */
@@ -507,6 +551,29 @@ int tts_vits_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t*
                     const float* d_logs_p, const float* d_noise, float noise_scale, int B, int C, int T_x, int T_y,
                     float* d_z_p, float* d_y_mask, float* d_m_p_out, float* d_logs_p_out, float* d_attn,
                     void* hip_stream);
+
+/* The rest of Vits.inference's glue on the device (since ABI 115).
+ * Given durations (vits.py:1141-1146): w = durations.unsqueeze(0); w_ceil [B][1][T_x] = ceil(w) (no
+ * mask, no length_scale), y_lengths [B] = max(sum(w_ceil), 1); durations [T_x] shared by every
+ * utterance (dur_bstride 0) or [B][T_x] (dur_bstride T_x). */
+int tts_vits_durations_given(const float* d_durations, int64_t dur_bstride, int B, int T_x, float* d_w_ceil,
+                             int64_t* d_y_lengths, void* hip_stream);
+/* (z * y_mask)[:, :, :T_out] (vits.py:1161): z [B][C][T] (batch stride C * T), y_mask [B][1][T],
+ * out [B][C][T_out], 1 <= T_out <= T. */
+int tts_vits_mask_slice(const float* d_z, const float* d_y_mask, int B, int C, int T, int T_out, float* d_out,
+                        void* hip_stream);
+/* upsampling_z (vits.py:944-959, encoder_sample_rate with interpolate_z): z2 [B][C][T2] =
+ * F.interpolate(z [B][C][T], scale_factor=[factor], mode="linear"), T2 = floor(T * factor);
+ * y_mask2 [B][1][T2] = sequence_mask(y_lengths * factor) (may be NULL).  The reference's product
+ * z2 * y_mask2 needs ceil(max(y_lengths) * factor) == T2; the caller checks it. */
+int tts_vits_upsample_z(const float* d_z, const int64_t* d_y_lengths, int B, int C, int T, double factor, int T2,
+                        float* d_z2, float* d_y_mask2, void* hip_stream);
+/* out [B][dim] = table[ids[b * id_stride]] (nn.Embedding rows: emb_g(sid), emb_l(lid)); ids are
+ * clamped to [0, num) (the reference raises IndexError; a device kernel cannot). */
+int tts_embedding_rows(const float* d_table, int num, int dim, const int64_t* d_ids, int64_t id_stride, int B,
+                       float* d_out, void* hip_stream);
+/* out [B][C] = d / max(||d||_2, 1e-12) per row (F.normalize(d_vectors), vits.py:884-886). */
+int tts_l2_normalize_rows(const float* d_in, int B, int C, float* d_out, void* hip_stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Single-op entry points (test / tuning surface).  These pack the host weights into a     */

@@ -20,6 +20,13 @@ fp64).  Follows Coqui TTS 0.22.0:
   w_ceil = ceil(w), y_lengths = clamp_min(sum(w_ceil), 1); generate_path
   (``TTS/tts/utils/helpers.py:154-169``); m_p / logs_p = attn^T m_p / logs_p;
   z_p = m_p + noise * exp(logs_p) * noise_scale (no y_mask)
+* language embeddings (YourTTS): the text encoder's cat(emb * sqrt(H), lang_emb.expand(T))
+  (networks.py:86-91) and the SDP's cond_lang (stochastic_duration_predictor.py:253-254)
+* ``TTS/tts/layers/glow_tts/duration_predictor.py:49-68``  the deterministic predictor VITS builds
+  with use_sdp=False (vits.py:694-702): x + cond(g) + cond_lang(lang), 2 x (conv -> relu ->
+  LayerNorm), proj, * mask
+* ``TTS/tts/models/vits.py:944-959``  upsampling_z: F.interpolate(z, scale_factor=[f], "linear"),
+  sequence_mask(y_lengths * f)
 
 Pinned against golden vectors of the reference modules (tests/golden/make_goldens.py vits_text).
 """
@@ -45,11 +52,14 @@ def _w(sd, dtype):
 
 def text_encoder(sd: Dict[str, torch.Tensor], tokens: torch.Tensor, lengths: torch.Tensor, hidden_channels: int = 192,
                  out_channels: int = 192, hidden_channels_ffn: int = 768, num_heads: int = 2, num_layers: int = 6,
-                 kernel_size: int = 3, dtype=torch.float64, **_unused):
-    """TextEncoder.forward (networks.py:83-100) -> (x, m, logs, x_mask)."""
+                 kernel_size: int = 3, dtype=torch.float64, lang_emb: Optional[torch.Tensor] = None, **_unused):
+    """TextEncoder.forward (networks.py:83-100) -> (x, m, logs, x_mask); lang_emb [B, L, 1] is
+    concatenated to every token's embedding (:90-91), the transformer then runs at H + L."""
     w = _w(sd, dtype)
     H = hidden_channels
     x = F.embedding(tokens, w["emb.weight"]) * math.sqrt(H)
+    if lang_emb is not None:
+        x = torch.cat((x, lang_emb.to(dtype).transpose(2, 1).expand(x.size(0), x.size(1), -1)), dim=-1)
     x = x.transpose(1, -1)
     x_mask = sequence_mask(lengths, x.size(2)).unsqueeze(1).to(dtype)
     ep = dict(kernel_size=kernel_size, num_layers=num_layers, num_heads=num_heads, hidden_channels_ffn=hidden_channels_ffn,
@@ -165,7 +175,8 @@ def conv_flow_reverse(w, pre: str, z, x_mask, g, hidden_channels: int, kernel_si
 
 def sdp_reverse(sd: Dict[str, torch.Tensor], x: torch.Tensor, x_mask: torch.Tensor, noise: torch.Tensor,
                 g: Optional[torch.Tensor] = None, noise_scale: float = 1.0, hidden_channels: int = 192,
-                kernel_size: int = 3, num_flows: int = 4, dtype=torch.float64, **_unused):
+                kernel_size: int = 3, num_flows: int = 4, dtype=torch.float64,
+                lang_emb: Optional[torch.Tensor] = None, **_unused):
     """StochasticDurationPredictor.forward(x, x_mask, g=g, reverse=True, noise_scale) with the noise
     torch.randn(B, 2, T) the reference draws at :277 given -> logw [B, 1, T]."""
     w = _w(sd, dtype)
@@ -174,6 +185,8 @@ def sdp_reverse(sd: Dict[str, torch.Tensor], x: torch.Tensor, x_mask: torch.Tens
     x = F.conv1d(x, w["pre.weight"], w["pre.bias"])
     if g is not None:
         x = x + F.conv1d(g.to(dtype), w["cond.weight"], w["cond.bias"])
+    if lang_emb is not None:  # :253-254
+        x = x + F.conv1d(lang_emb.to(dtype), w["cond_lang.weight"], w["cond_lang.bias"])
     x = dds_conv(w, "convs", x, x_mask, 3, kernel_size)
     x = F.conv1d(x, w["proj.weight"], w["proj.bias"]) * x_mask
     z = noise.to(dtype) * noise_scale
@@ -209,3 +222,34 @@ def vits_expand(w_ceil, x_mask, y_lengths, m_p, logs_p, noise=None, noise_scale:
         noise = torch.zeros_like(mp)
     z_p = mp + noise.to(mp.dtype) * torch.exp(lp) * noise_scale
     return z_p, y_mask, mp, lp, attn
+
+
+def dp_forward(sd: Dict[str, torch.Tensor], x: torch.Tensor, x_mask: torch.Tensor, g: Optional[torch.Tensor] = None,
+               lang_emb: Optional[torch.Tensor] = None, kernel_size: int = 3, dtype=torch.float64, **_unused):
+    """DurationPredictor.forward (glow_tts/duration_predictor.py:49-68; dropout is identity at eval)
+    -> logw [B, 1, T]."""
+    from .glow_tts_ref import layer_norm
+
+    w = _w(sd, dtype)
+    x = x.to(dtype)
+    x_mask = x_mask.to(dtype)
+    if g is not None:
+        x = x + F.conv1d(g.to(dtype), w["cond.weight"], w["cond.bias"])
+    if lang_emb is not None:
+        x = x + F.conv1d(lang_emb.to(dtype), w["cond_lang.weight"], w["cond_lang.bias"])
+    x = F.conv1d(x * x_mask, w["conv_1.weight"], w["conv_1.bias"], padding=kernel_size // 2)
+    x = layer_norm(torch.relu(x), w["norm_1.gamma"], w["norm_1.beta"])
+    x = F.conv1d(x * x_mask, w["conv_2.weight"], w["conv_2.bias"], padding=kernel_size // 2)
+    x = layer_norm(torch.relu(x), w["norm_2.gamma"], w["norm_2.beta"])
+    x = F.conv1d(x * x_mask, w["proj.weight"], w["proj.bias"])
+    return x * x_mask
+
+
+def upsample_z(z: torch.Tensor, y_lengths: torch.Tensor, factor: float):
+    """Vits.upsampling_z (vits.py:944-959) with encoder_sample_rate and interpolate_z:
+    (F.interpolate(z, scale_factor=[factor], mode="linear"), sequence_mask(y_lengths * factor))."""
+    z2 = F.interpolate(z, scale_factor=[factor], mode="linear")
+    lens = y_lengths * factor  # long * python float -> float32 lengths
+    seq = torch.arange(lens.max(), dtype=lens.dtype)  # helpers.sequence_mask: arange of a float max
+    y_mask = (seq[None, :] < lens[:, None]).to(z.dtype).unsqueeze(1)
+    return z2, y_mask

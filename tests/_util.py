@@ -20,8 +20,11 @@ FP32_MAX_ABS = 1e-4
 FP32_REL_RMS = 5e-6
 WAV_MAX_ABS = 1e-5
 # bf16 math mode (TTS_MATH_BF16, configs 3 / 5): SURVEY.md §8c's bf16 gate; the reference's own
-# bf16 CPU forward measured rel-RMS 1.3e-2 and max 6.2e-3 vs fp64
-BF16_MAX_ABS = 1e-1
+# bf16 CPU forward measured rel-RMS 1.3e-2 and max 6.2e-3 vs fp64.  max|d|: 5e-2 on waveforms and
+# flow latents (the worst measured in the round-5 log is 0.027, profiles/parity_errors_r05.jsonl),
+# 1e-1 on unbounded outputs (single ops, the posterior's z = m + eps * exp(logs): 0.060)
+BF16_MAX_ABS = 5e-2
+BF16_MAX_ABS_OP = 1e-1
 BF16_REL_RMS = 3e-2
 
 
@@ -29,7 +32,7 @@ def tol(mode: str, op: bool = False) -> dict:
     """Parity gates of a math mode (every mode but bf16 is held to the fp32 gates); ``op``:
     a single conv's output (magnitude not bounded like a waveform's)."""
     if mode == "bf16":
-        return dict(max_abs_tol=BF16_MAX_ABS, rel_rms_tol=BF16_REL_RMS)
+        return dict(max_abs_tol=BF16_MAX_ABS_OP if op else BF16_MAX_ABS, rel_rms_tol=BF16_REL_RMS)
     return dict(max_abs_tol=FP32_MAX_ABS if op else WAV_MAX_ABS, rel_rms_tol=FP32_REL_RMS)
 
 

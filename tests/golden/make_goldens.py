@@ -26,6 +26,7 @@ import types
 
 import numpy as np
 import torch
+from torch.nn.functional import embedding as F_embedding
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -338,22 +339,43 @@ def import_reference_vits_text():
     return TextEncoder, StochasticDurationPredictor, ResidualCouplingBlocks, HifiganGenerator, generate_path, sequence_mask
 
 
-def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok_seed, gin=0):
+def import_reference_duration_predictor():
+    import_reference()
+    from TTS.tts.layers.glow_tts.duration_predictor import DurationPredictor
+
+    return DurationPredictor
+
+
+def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok_seed, gin=0, lang=0, lids=None,
+                   use_sdp=True, up_factor=None):
     """G14: Vits.inference (vits.py:1121-1162) tokens -> waveform through the reference's TextEncoder,
     StochasticDurationPredictor(reverse=True), generate_path / sequence_mask, ResidualCouplingBlocks
     and HifiganGenerator.  Vits itself imports torchaudio / librosa / coqpit (absent), so the glue's
     lines are restated here around the reference modules.  Both noise draws (the SDP's torch.randn
     at stochastic_duration_predictor.py:277 and randn_like(m_p) at vits.py:1154) are made here with
     fixed seeds and stored; the fp64 run reuses them.  gin > 0: a speaker vector g [B, gin, 1] drawn
-    and stored, fed to the SDP (condition_dp_on_speaker), the flow and the decoder as vits.py does."""
+    and stored, fed to the SDP (condition_dp_on_speaker), the flow and the decoder as vits.py does.
+    lang > 0 (YourTTS, vits.py:796-801, :1119-1124): an emb_l table [3, lang] and per-utterance ids
+    ``lids`` stored, lang_emb = emb_l(lid).unsqueeze(-1) into the TextEncoder (language_emb_dim) and the
+    duration predictor.  use_sdp False: the reference's glow_tts DurationPredictor(H, 256, 3, 0.5,
+    cond_channels=gin, language_emb_dim=lang) (vits.py:694-702, :1136-1139).  up_factor: upsampling_z
+    (vits.py:944-959) with interpolate_factor = up_factor, restated around the reference's own
+    sequence_mask (Vits imports torchaudio)."""
     TextEncoder, SDP, RCB, HifiganGenerator, generate_path, sequence_mask = refs
     torch.manual_seed(0)
     te = TextEncoder(tcfg["num_chars"], tcfg["out_channels"], tcfg["hidden_channels"], tcfg["hidden_channels_ffn"],
-                     tcfg["num_heads"], tcfg["num_layers"], tcfg["kernel_size"], 0.1)
-    te.load_state_dict(synthetic.vits_text_encoder_state_dict(**tcfg, seed=seeds[0]))
-    dp = SDP(scfg["in_channels"], scfg["hidden_channels"], scfg["kernel_size"], 0.5, scfg["num_flows"],
-             cond_channels=gin)
-    dp.load_state_dict(synthetic.vits_sdp_state_dict(**scfg, cond_channels=gin, seed=seeds[1]))
+                     tcfg["num_heads"], tcfg["num_layers"], tcfg["kernel_size"], 0.1, language_emb_dim=lang or None)
+    te.load_state_dict(synthetic.vits_text_encoder_state_dict(**tcfg, language_emb_dim=lang, seed=seeds[0]))
+    if use_sdp:
+        dp = SDP(scfg["in_channels"], scfg["hidden_channels"], scfg["kernel_size"], 0.5, scfg["num_flows"],
+                 cond_channels=gin, language_emb_dim=lang)
+        dp.load_state_dict(synthetic.vits_sdp_state_dict(**dict(scfg, in_channels=scfg["in_channels"] + lang),
+                                                         cond_channels=gin, language_emb_dim=lang, seed=seeds[1]))
+    else:
+        DP = import_reference_duration_predictor()
+        dp = DP(tcfg["hidden_channels"], 256, 3, 0.5, cond_channels=gin, language_emb_dim=lang)
+        dp.load_state_dict(synthetic.vits_dp_state_dict(tcfg["hidden_channels"], 256, 3, cond_channels=gin,
+                                                        language_emb_dim=lang, seed=seeds[1]))
     fl = RCB(fcfg["channels"], fcfg["hidden_channels"], fcfg["kernel_size"], fcfg["dilation_rate"], fcfg["num_layers"],
              num_flows=fcfg["num_flows"], cond_channels=gin)
     fl.load_state_dict(synthetic.vits_flow_state_dict(**dict(fcfg, cond_channels=gin), seed=seeds[2]))
@@ -366,20 +388,26 @@ def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok
     gen = torch.Generator().manual_seed(tok_seed + 300)
     g = torch.randn(B, gin, 1, generator=gen) if gin else None
     noise_dp = torch.randn(B, 2, T, generator=gen)
+    emb_l = torch.randn(3, lang, generator=gen) if lang else None
+    lang_emb = F_embedding(torch.tensor(lids), emb_l).unsqueeze(-1) if lang else None  # emb_l(lid).unsqueeze(-1)
     ns, ls, ns_dp = 0.667, 1.0, 1.0  # VitsArgs inference_noise_scale, length_scale, inference_noise_scale_dp
 
     def infer(dtype, noise_z):
         mods = [m.to(dtype) for m in (te, dp, fl, dec)]
         gg = g.to(dtype) if g is not None else None
+        le = lang_emb.to(dtype) if lang_emb is not None else None
         with torch.no_grad():
-            x, m_p, logs_p, x_mask = mods[0](tok, lens)
-            # the SDP's own draw replaced by the stored one (torch.randn(x.size(0), 2, x.size(2)))
-            orig = torch.randn
-            torch.randn = lambda *a, **k: noise_dp.clone()
-            try:
-                logw = mods[1](x, x_mask, g=gg, reverse=True, noise_scale=ns_dp)
-            finally:
-                torch.randn = orig
+            x, m_p, logs_p, x_mask = mods[0](tok, lens, lang_emb=le)
+            if use_sdp:
+                # the SDP's own draw replaced by the stored one (torch.randn(x.size(0), 2, x.size(2)))
+                orig = torch.randn
+                torch.randn = lambda *a, **k: noise_dp.clone()
+                try:
+                    logw = mods[1](x, x_mask, g=gg, reverse=True, noise_scale=ns_dp, lang_emb=le)
+                finally:
+                    torch.randn = orig
+            else:
+                logw = mods[1](x, x_mask, g=gg, lang_emb=le)
             w = torch.exp(logw) * x_mask * ls
             w_ceil = torch.ceil(w)
             y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
@@ -392,6 +420,9 @@ def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok
                 noise_z = torch.randn(mp.shape, generator=torch.Generator().manual_seed(tok_seed + 301))
             z_p = mp + noise_z.to(dtype) * torch.exp(lp) * ns
             z = mods[2](z_p, y_mask, g=gg, reverse=True)
+            if up_factor:  # upsampling_z (vits.py:951-957)
+                z = torch.nn.functional.interpolate(z, scale_factor=[up_factor], mode="linear").squeeze(0)
+                y_mask = sequence_mask(y_lengths * up_factor, None).to(y_mask.dtype).unsqueeze(1)
             wav = mods[3](z * y_mask, g=gg)
         out = dict(x=x, m_p=m_p, logs_p=logs_p, x_mask=x_mask, logw=logw, w=w, w_ceil=w_ceil, y_lengths=y_lengths,
                    y_mask=y_mask, attn=attn, m_p_exp=mp, logs_p_exp=lp, z_p=z_p, z=z, wav=wav)
@@ -404,6 +435,10 @@ def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok
     arrays = dict(tokens=tok.numpy(), lengths=lens.numpy(), noise_dp=noise_dp.numpy(), noise_z=noise_z.numpy())
     if g is not None:
         arrays["g"] = g.numpy()
+    if lang:
+        arrays["emb_l"] = emb_l.numpy()
+        arrays["lids"] = np.asarray(lids, np.int64)
+        arrays["lang_emb"] = lang_emb.numpy()
     for k, v in o32.items():
         arrays[f"{k}_ref_fp32"] = v.numpy()
     for k, v in o64.items():
@@ -413,7 +448,7 @@ def vits_text_case(refs, name, tcfg, scfg, fcfg, dcfg, seeds, B, T, lengths, tok
     margin = float(np.minimum(frac, 1 - frac).min())
     meta = dict(kind="vits_text", text_encoder=tcfg, sdp=scfg, flow=fcfg, decoder=dcfg, seeds=list(seeds),
                 tok_seed=tok_seed, B=B, T=T, lengths=lengths, gin=gin, noise_scale=ns, length_scale=ls,
-                noise_scale_dp=ns_dp, ceil_margin=margin)
+                noise_scale_dp=ns_dp, ceil_margin=margin, lang=lang, use_sdp=use_sdp, up_factor=up_factor)
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, meta=json.dumps(meta), **arrays)
     print(f"wrote {path}: y_lengths {o32['y_lengths'].tolist()} wav {tuple(o32['wav'].shape)} ceil margin "
@@ -435,6 +470,13 @@ def main_vits_text():
                    lengths=[13, 8, 1], tok_seed=51)
     vits_text_case(refs, "vits_text_spk_b2_t11", tcfg, dict(VITS_SDP), fcfg, dcfg, (7532, 9754, 2471, 102), B=2,
                    T=11, lengths=[11, 6], tok_seed=52, gin=16)
+    if len(sys.argv) > 2 and sys.argv[2] == "r6":  # round 6: the remaining VitsArgs switches
+        # YourTTS language embeddings (4 channels, 3 languages) through the SDP
+        vits_text_case(refs, "vits_text_lang_b3_t13", tcfg, dict(VITS_SDP), fcfg, dcfg, (7533, 9755, 2472, 103), B=3,
+                       T=13, lengths=[13, 9, 4], tok_seed=53, lang=4, lids=[2, 0, 1])
+        # use_sdp=False with speaker + language conditioning, and upsampling_z x2 (44.1 kHz from 22.05 kHz)
+        vits_text_case(refs, "vits_text_dp_up_b2_t11", tcfg, dict(VITS_SDP), fcfg, dcfg, (7534, 4712, 2473, 104), B=2,
+                       T=11, lengths=[11, 7], tok_seed=54, gin=16, lang=4, lids=[1, 2], use_sdp=False, up_factor=2.0)
 
 
 def main_vits_posterior():

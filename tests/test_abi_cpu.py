@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_target():
-    assert N.lib().tts_abi_version() == N.ABI_VERSION == 114
+    assert N.lib().tts_abi_version() == N.ABI_VERSION == 115
     assert N.lib().tts_build_target() == b"gfx950"
     assert N.lib().tts_last_error() == b""
 
@@ -482,8 +482,32 @@ def test_vits_text_weight_inventories_match_modules():
             assert w.size == N.lib().tts_vits_sdp_weight_numel(ctypes.byref(sdp._cfg), i), i
     c = N.TtsVitsSdpCfg(192, 192, 3, 4, 0, 0, N.MATH_MODES["f16x3"])
     assert N.lib().tts_vits_sdp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
-    c = N.TtsVitsSdpCfg(192, 192, 3, 4, 0, 8, N.MATH_MODES["fp32"])  # language embeddings
-    assert N.lib().tts_vits_sdp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    # language embeddings (ABI 115): the text encoder at H + L, the SDP's cond_lang
+    te = TextEncoder(64, 192, 192, 768, 2, 6, 3, 0.1, language_emb_dim=4)
+    ws = te._weight_list()
+    assert ws[0].size == 64 * 192 and ws[1].size == 196 * 196  # emb at H, the transformer at H + L
+    assert len(ws) == N.lib().tts_vits_text_encoder_num_weights(ctypes.byref(te._cfg))
+    for i, w in enumerate(ws):
+        assert w.size == N.lib().tts_vits_text_encoder_weight_numel(ctypes.byref(te._cfg), i), i
+    for gin, L in ((0, 4), (16, 4)):
+        sdp = StochasticDurationPredictor(192, 192, 3, 0.5, 4, cond_channels=gin, language_emb_dim=L)
+        ws = sdp._weight_list()
+        assert len(ws) == N.lib().tts_vits_sdp_num_weights(ctypes.byref(sdp._cfg))
+        for i, w in enumerate(ws):
+            assert w.size == N.lib().tts_vits_sdp_weight_numel(ctypes.byref(sdp._cfg), i), i
+    # the deterministic duration predictor (use_sdp=False), every conditioning combination
+    from tts_amd.tts import DurationPredictor
+
+    for gin, L in ((0, 0), (16, 0), (0, 4), (16, 4)):
+        dp = DurationPredictor(192, 256, 3, 0.5, cond_channels=gin, language_emb_dim=L)
+        ws = dp._weight_list()
+        assert len(ws) == N.lib().tts_vits_dp_num_weights(ctypes.byref(dp._cfg)) == 10 + 2 * bool(gin) + 2 * bool(L)
+        for i, w in enumerate(ws):
+            assert w.size == N.lib().tts_vits_dp_weight_numel(ctypes.byref(dp._cfg), i), i
+    c = N.TtsVitsDpCfg(192, 256, 3, 0, 0, N.MATH_MODES["f16x3"])
+    assert N.lib().tts_vits_dp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
+    c = N.TtsVitsDpCfg(192, 256, 4, 0, 0, N.MATH_MODES["fp32"])  # even kernel
+    assert N.lib().tts_vits_dp_num_weights(ctypes.byref(c)) == -N.TTS_ERR_UNSUPPORTED
     t = N.TtsVitsTextEncoderCfg(64, 192, 192, 768, 3, 6, 3, 0, 0)  # 192 % 3 == 0 but dk = 64: fine
     assert N.lib().tts_vits_text_encoder_num_weights(ctypes.byref(t)) > 0
     t = N.TtsVitsTextEncoderCfg(64, 192, 192, 768, 5, 6, 3, 0, 0)  # channels not divisible by heads

@@ -659,3 +659,22 @@ def test_whole_block_k7_k11_matches_pairs(cuda_device, monkeypatch, mode):
             for nm in ("mrf_block_k7_c32", "mrf_block_k11_c32", "mrf_block_k7_c64", "mrf_block_k11_c64"):
                 assert names.count(nm) == 1, (nm, names)
     assert max_abs(outs[0].numpy(), outs[1].numpy()) <= 2 * tol(mode).get("max_abs_tol", 1e-4)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "f16x3"])
+def test_nonfinite_mel_stays_in_its_utterance(cuda_device, mode):
+    """A NaN / inf mel value is outside the generator's contract (the kernels build without NaN
+    semantics, include/tts_mi355x.h), but it must not leak: every other utterance of the batch is
+    bitwise the clean run's (per-utterance planes and f16x3 statistics, split over lanes)."""
+    sd = synthetic.hifigan_state_dict(seed=1234, weight_norm=False)
+    g = HifiganGenerator(**V1, math_mode=mode)
+    g.remove_weight_norm()
+    g.load_state_dict(sd)
+    g = g.to(cuda_device)
+    mel = synthetic.mel(3, 40, seed=5).to(cuda_device)
+    clean = g.inference(mel)
+    for bad_value in (float("nan"), float("inf")):
+        bad = mel.clone()
+        bad[1, 7, 20] = bad_value
+        out = g.inference(bad)
+        assert torch.equal(out[0], clean[0]) and torch.equal(out[2], clean[2]), bad_value

@@ -288,43 +288,42 @@ VTEXT = goldens("vits_text")
 @pytest.mark.parametrize("name,meta,arr", VTEXT, ids=[g[0] for g in VTEXT])
 def test_vits_text_oracle_matches_reference(name, meta, arr):
     """oracle/vits_text_ref.py against the reference's Vits.inference chain (make_goldens.py
-    vits_text): TextEncoder, SDP reverse with the stored noise, the duration glue, then the flow
-    and decoder oracles close it to the waveform (fp64 throughout)."""
+    vits_text): TextEncoder (with the language embedding concatenated when the fixture has one), the
+    SDP reverse with the stored noise or the deterministic DurationPredictor (use_sdp=False), the
+    duration glue, the flow, upsampling_z when recorded, and the decoder (fp64 throughout)."""
+    from _vits_chain import oracle_chain, state_dicts
     from oracle import vits_text_ref
 
-    tcfg, scfg, gin = meta["text_encoder"], meta["sdp"], meta["gin"]
-    tsd = synthetic.vits_text_encoder_state_dict(**tcfg, seed=meta["seeds"][0])
-    tok, lens = torch.from_numpy(arr["tokens"]), torch.from_numpy(arr["lengths"])
-    x, m, logs, xm = vits_text_ref.text_encoder(tsd, tok, lens, dtype=torch.float64, **tcfg)
-    for n, o in (("x", x), ("m_p", m), ("logs_p", logs), ("x_mask", xm)):
-        assert max_abs(o.numpy(), arr[f"{n}_ref_fp64"]) < 1e-10, n
-    g = torch.from_numpy(arr["g"]).double() if gin else None
-    ssd = synthetic.vits_sdp_state_dict(**scfg, cond_channels=gin, seed=meta["seeds"][1])
-    logw = vits_text_ref.sdp_reverse(ssd, x, xm, torch.from_numpy(arr["noise_dp"]), g=g,
-                                     noise_scale=meta["noise_scale_dp"], dtype=torch.float64, **scfg)
-    assert max_abs(logw.numpy(), arr["logw_ref_fp64"]) < 1e-10
-    w_ceil, y_len = vits_text_ref.vits_durations(logw, xm, meta["length_scale"])
-    assert torch.equal(w_ceil, torch.from_numpy(arr["w_ceil_ref_fp64"]))
-    assert torch.equal(y_len, torch.from_numpy(arr["y_lengths_ref_fp64"]))
-    z_p, y_mask, mp, lp, attn = vits_text_ref.vits_expand(w_ceil, xm, y_len, m, logs, torch.from_numpy(arr["noise_z"]),
-                                                          meta["noise_scale"])
-    assert torch.equal(attn, torch.from_numpy(arr["attn_ref_fp64"]))
-    assert torch.equal(y_mask, torch.from_numpy(arr["y_mask_ref_fp64"]))
-    assert max_abs(mp.numpy(), arr["m_p_exp_ref_fp64"]) < 1e-12
-    assert max_abs(z_p.numpy(), arr["z_p_ref_fp64"]) < 1e-12
-    fcfg = dict(meta["flow"], cond_channels=gin)
-    fsd = synthetic.vits_flow_state_dict(**fcfg, seed=meta["seeds"][2])
-    z = vits_ref.vits_flow_reverse(fsd, z_p, y_mask, g=g, dtype=torch.float64, **fcfg)
-    assert max_abs(z.numpy(), arr["z_ref_fp64"]) < 1e-10
-    dcfg = dict(meta["decoder"], cond_channels=gin)
-    dsd = synthetic.hifigan_state_dict(**dcfg, seed=meta["seeds"][3], weight_norm=True)
-    wav = hifigan_ref.hifigan_forward(dsd, z * y_mask, pad=0, g=g, dtype=torch.float64, fold_dtype=torch.float64,
-                                      **dcfg)
-    assert max_abs(wav.numpy(), arr["wav_ref_fp64"]) < 1e-10
+    o = oracle_chain(meta, arr)
+    for n in ("x", "m_p", "logs_p", "x_mask", "logw"):
+        assert max_abs(o[n].numpy(), arr[f"{n}_ref_fp64"]) < 1e-10, n
+    assert torch.equal(o["w_ceil"], torch.from_numpy(arr["w_ceil_ref_fp64"]))
+    assert torch.equal(o["y_lengths"], torch.from_numpy(arr["y_lengths_ref_fp64"]))
+    assert torch.equal(o["attn"], torch.from_numpy(arr["attn_ref_fp64"]))
+    assert max_abs(o["m_p_exp"].numpy(), arr["m_p_exp_ref_fp64"]) < 1e-12
+    assert max_abs(o["z_p"].numpy(), arr["z_p_ref_fp64"]) < 1e-12
+    assert torch.equal(o.get("y_mask_up", o["y_mask"]), torch.from_numpy(arr["y_mask_ref_fp64"]))
+    assert max_abs(o["z"].numpy(), arr["z_ref_fp64"]) < 1e-10
+    assert max_abs(o["wav"].numpy(), arr["wav_ref_fp64"]) < 1e-10
     # fp32 oracle vs the reference's fp32 run, and the duration ceil() margin
-    x32, m32, _, _ = vits_text_ref.text_encoder(tsd, tok, lens, dtype=torch.float32, **tcfg)
+    tsd = state_dicts(meta)[0]
+    le = torch.from_numpy(arr["lang_emb"]) if meta.get("lang") else None
+    x32, _, _, _ = vits_text_ref.text_encoder(tsd, torch.from_numpy(arr["tokens"]), torch.from_numpy(arr["lengths"]),
+                                              dtype=torch.float32, lang_emb=le, **meta["text_encoder"])
     assert max_abs(x32.numpy(), arr["x_ref_fp32"]) < 1e-4
     assert meta["ceil_margin"] > 1e-3
+
+
+def test_vits_upsample_z_oracle_matches_interpolate():
+    """upsample_z at non-integer factors: the same F.interpolate call and the float-length sequence
+    mask (helpers.sequence_mask on y_lengths * factor) as vits.py:951-957."""
+    from oracle import vits_text_ref
+
+    z = torch.randn(2, 3, 10, generator=torch.Generator().manual_seed(3))
+    for f in (2.0, 1.5, 3.0):
+        z2, m = vits_text_ref.upsample_z(z, torch.tensor([10, 7]), f)
+        assert z2.shape[2] == int(10 * f) and m.shape == (2, 1, int(10 * f))
+        assert m[1, 0].sum() == np.ceil(7 * f)
 
 
 def test_rq_spline_inverse_roundtrip():

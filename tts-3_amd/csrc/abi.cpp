@@ -1,5 +1,6 @@
 // extern "C" entry points of libtts_mi355x.so (declared in include/tts_mi355x.h).
 // Every call converts library exceptions into a status code + thread-local message.
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -69,7 +70,7 @@ struct TmpDev {
 extern "C" {
 
 const char* tts_last_error(void) { return g_last_error.c_str(); }
-int tts_abi_version(void) { return 114; }
+int tts_abi_version(void) { return 115; }
 const char* tts_build_target(void) { return "gfx950"; }
 
 // ----------------------------------------------------------------------------- HiFiGAN
@@ -281,19 +282,20 @@ int tts_vits_text_encoder_destroy(void* handle) {
   return guarded([&] { delete static_cast<tts::VitsTextEncoder*>(handle); });
 }
 
-int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B, int T,
-                                  float* d_x, float* d_m, float* d_logs, float* d_x_mask, void* hip_stream) {
+int tts_vits_text_encoder_forward(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                  const float* d_lang_emb, int B, int T, float* d_x, float* d_m, float* d_logs,
+                                  float* d_x_mask, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
-    static_cast<tts::VitsTextEncoder*>(handle)->forward(d_tokens, d_lengths, B, T, d_x, d_m, d_logs, d_x_mask,
-                                                        static_cast<hipStream_t>(hip_stream));
+    static_cast<tts::VitsTextEncoder*>(handle)->forward(d_tokens, d_lengths, d_lang_emb, B, T, d_x, d_m, d_logs,
+                                                        d_x_mask, static_cast<hipStream_t>(hip_stream));
   });
 }
 
-int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths, int B,
-                                           int T, float* d_x, float* d_m, float* d_logs, float* d_x_mask,
-                                           void* hip_stream, TtsLaunchRecord* records, int max_records,
-                                           int* n_records) {
+int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens, const int64_t* d_lengths,
+                                           const float* d_lang_emb, int B, int T, float* d_x, float* d_m,
+                                           float* d_logs, float* d_x_mask, void* hip_stream,
+                                           TtsLaunchRecord* records, int max_records, int* n_records) {
   return guarded([&] {
     TTS_REQUIRE(handle && n_records, 1, "NULL argument");
     auto* h = static_cast<tts::VitsTextEncoder*>(handle);
@@ -301,7 +303,7 @@ int tts_vits_text_encoder_forward_profiled(void* handle, const int64_t* d_tokens
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->forward(d_tokens, d_lengths, B, T, d_x, d_m, d_logs, d_x_mask, s, &prof);
+      h->forward(d_tokens, d_lengths, d_lang_emb, B, T, d_x, d_m, d_logs, d_x_mask, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);
@@ -342,18 +344,20 @@ int tts_vits_sdp_destroy(void* handle) {
   return guarded([&] { delete static_cast<tts::VitsSdp*>(handle); });
 }
 
-int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g, const float* d_noise,
-                         float noise_scale, int B, int T, float* d_logw, void* hip_stream) {
+int tts_vits_sdp_reverse(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                         const float* d_lang_emb, const float* d_noise, float noise_scale, int B, int T,
+                         float* d_logw, void* hip_stream) {
   return guarded([&] {
     TTS_REQUIRE(handle, 1, "NULL handle");
-    static_cast<tts::VitsSdp*>(handle)->reverse(d_x, d_x_mask, d_g, d_noise, noise_scale, B, T, d_logw,
+    static_cast<tts::VitsSdp*>(handle)->reverse(d_x, d_x_mask, d_g, d_lang_emb, d_noise, noise_scale, B, T, d_logw,
                                                 static_cast<hipStream_t>(hip_stream));
   });
 }
 
 int tts_vits_sdp_reverse_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
-                                  const float* d_noise, float noise_scale, int B, int T, float* d_logw,
-                                  void* hip_stream, TtsLaunchRecord* records, int max_records, int* n_records) {
+                                  const float* d_lang_emb, const float* d_noise, float noise_scale, int B, int T,
+                                  float* d_logw, void* hip_stream, TtsLaunchRecord* records, int max_records,
+                                  int* n_records) {
   return guarded([&] {
     TTS_REQUIRE(handle && n_records, 1, "NULL argument");
     auto* h = static_cast<tts::VitsSdp*>(handle);
@@ -361,7 +365,67 @@ int tts_vits_sdp_reverse_profiled(void* handle, const float* d_x, const float* d
     tts::Profiler prof;
     {
       tts::DeviceGuard g(h->device());
-      h->reverse(d_x, d_x_mask, d_g, d_noise, noise_scale, B, T, d_logw, s, &prof);
+      h->reverse(d_x, d_x_mask, d_g, d_lang_emb, d_noise, noise_scale, B, T, d_logw, s, &prof);
+      TTS_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    export_records(prof, records, max_records, n_records);
+  });
+}
+
+int tts_vits_dp_num_weights(const TtsVitsDpCfg* cfg) {
+  int n = -1;
+  int st = guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_dp_validate(*cfg);
+    n = (int)tts::vits_dp_weight_shapes(*cfg).size();
+  });
+  return st == TTS_OK ? n : -st;
+}
+
+int64_t tts_vits_dp_weight_numel(const TtsVitsDpCfg* cfg, int idx) {
+  int64_t n = -1;
+  guarded([&] {
+    TTS_REQUIRE(cfg, 1, "NULL cfg");
+    tts::vits_dp_validate(*cfg);
+    auto s = tts::vits_dp_weight_shapes(*cfg);
+    TTS_REQUIRE(idx >= 0 && idx < (int)s.size(), 1, "weight index out of range");
+    n = s[idx];
+  });
+  return n;
+}
+
+int tts_vits_dp_create(const TtsVitsDpCfg* cfg, const float* const* host_weights, int device, void** handle) {
+  return guarded([&] {
+    TTS_REQUIRE(cfg && host_weights && handle, 1, "NULL argument");
+    *handle = nullptr;
+    *handle = new tts::VitsDp(*cfg, host_weights, device);
+  });
+}
+
+int tts_vits_dp_destroy(void* handle) {
+  return guarded([&] { delete static_cast<tts::VitsDp*>(handle); });
+}
+
+int tts_vits_dp_forward(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                        const float* d_lang_emb, int B, int T, float* d_logw, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(handle, 1, "NULL handle");
+    static_cast<tts::VitsDp*>(handle)->forward(d_x, d_x_mask, d_g, d_lang_emb, B, T, d_logw,
+                                               static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_dp_forward_profiled(void* handle, const float* d_x, const float* d_x_mask, const float* d_g,
+                                 const float* d_lang_emb, int B, int T, float* d_logw, void* hip_stream,
+                                 TtsLaunchRecord* records, int max_records, int* n_records) {
+  return guarded([&] {
+    TTS_REQUIRE(handle && n_records, 1, "NULL argument");
+    auto* h = static_cast<tts::VitsDp*>(handle);
+    auto s = static_cast<hipStream_t>(hip_stream);
+    tts::Profiler prof;
+    {
+      tts::DeviceGuard g(h->device());
+      h->forward(d_x, d_x_mask, d_g, d_lang_emb, B, T, d_logw, s, &prof);
       TTS_HIP_CHECK(hipStreamSynchronize(s));
     }
     export_records(prof, records, max_records, n_records);
@@ -394,6 +458,50 @@ int tts_vits_expand(const float* d_w_ceil, const float* d_x_mask, const int64_t*
     a.vits = 1;
     tts::launch_expand(a, B, static_cast<hipStream_t>(hip_stream));
     TTS_HIP_CHECK(hipGetLastError());
+  });
+}
+
+int tts_vits_durations_given(const float* d_durations, int64_t dur_bstride, int B, int T_x, float* d_w_ceil,
+                             int64_t* d_y_lengths, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_durations && d_w_ceil && d_y_lengths, 1, "NULL argument");
+    TTS_REQUIRE(B >= 1 && T_x >= 1 && (dur_bstride == 0 || dur_bstride >= T_x), 1, "bad durations shape");
+    tts::launch_given_durations(d_durations, dur_bstride, d_w_ceil, d_y_lengths, B, T_x,
+                                static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_mask_slice(const float* d_z, const float* d_y_mask, int B, int C, int T, int T_out, float* d_out,
+                        void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_z && d_y_mask && d_out, 1, "NULL argument");
+    tts::launch_mask_slice(d_z, d_y_mask, d_out, B, C, T, T_out, static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_vits_upsample_z(const float* d_z, const int64_t* d_y_lengths, int B, int C, int T, double factor, int T2,
+                        float* d_z2, float* d_y_mask2, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_z && d_z2 && (d_y_lengths || !d_y_mask2), 1, "NULL argument");
+    TTS_REQUIRE(factor > 0.0 && T2 == (int)std::floor((double)T * factor), 1,
+                "upsample_z: T2 must be floor(T * factor) (F.interpolate's output length)");
+    tts::launch_upsample_z(d_z, d_y_lengths, d_z2, d_y_mask2, B, C, T, T2, factor,
+                           static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_embedding_rows(const float* d_table, int num, int dim, const int64_t* d_ids, int64_t id_stride, int B,
+                       float* d_out, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_table && d_ids && d_out, 1, "NULL argument");
+    tts::launch_embedding_rows(d_table, d_ids, id_stride, d_out, B, dim, num, static_cast<hipStream_t>(hip_stream));
+  });
+}
+
+int tts_l2_normalize_rows(const float* d_in, int B, int C, float* d_out, void* hip_stream) {
+  return guarded([&] {
+    TTS_REQUIRE(d_in && d_out, 1, "NULL argument");
+    tts::launch_l2_normalize(d_in, d_out, B, C, static_cast<hipStream_t>(hip_stream));
   });
 }
 

@@ -26,11 +26,11 @@ constexpr double kBnEps = 1e-5;  // nn.BatchNorm1d default
 int odd_k(int k) { return k % 2 ? k : k + 1; }
 }  // namespace
 
-std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp) {
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp, int emb_channels) {
   std::vector<int64_t> n;
   const int64_t H = c.hidden_channels, F = c.hidden_channels_ffn, K = c.kernel_size, D = c.hidden_channels_dp;
   const int et = c.encoder_type;
-  n.push_back((int64_t)c.num_chars * H);  // emb.weight
+  n.push_back((int64_t)c.num_chars * (emb_channels > 0 ? emb_channels : H));  // emb.weight
   auto bn = [&](int64_t C) { for (int i = 0; i < 4; ++i) n.push_back(C); };
   if (c.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {
     for (int l = 0; l < 3; ++l) {
@@ -120,11 +120,16 @@ void glow_encoder_validate(const TtsGlowEncoderCfg& c) {
               "Glow encoder: math_mode FP32_F16X3 is not implemented (use FP32, FP32_X6 or BF16)");
 }
 
-GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, int device, bool with_dp)
-    : cfg_(cfg), device_(device), with_dp_(with_dp) {
+GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, int device, bool with_dp,
+                         int emb_channels)
+    : cfg_(cfg), device_(device), with_dp_(with_dp),
+      emb_ch_(emb_channels > 0 ? emb_channels : cfg.hidden_channels) {
   glow_encoder_validate(cfg_);
+  TTS_REQUIRE(emb_ch_ <= cfg_.hidden_channels && (emb_ch_ == cfg_.hidden_channels ||
+                                                  cfg_.encoder_type == TTS_ENC_REL_POS_TRANSFORMER),
+              1, "Glow encoder: embedding narrower than the encoder only for the relative-position transformer");
   DeviceGuard g(device_);
-  const auto shapes = glow_encoder_weight_shapes(cfg_, with_dp_);
+  const auto shapes = glow_encoder_weight_shapes(cfg_, with_dp_, emb_ch_);
   for (size_t i = 0; i < shapes.size(); ++i)
     TTS_REQUIRE(hw[i] != nullptr, 1, "weight pointer " + std::to_string(i) + " is NULL");
   const int H = cfg_.hidden_channels, F = cfg_.hidden_channels_ffn, K = cfg_.kernel_size;
@@ -201,7 +206,7 @@ GlowEncoder::GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* hw, i
   const int et = cfg_.encoder_type;
 
   size_t wi = 0;
-  put(hw[wi++], (size_t)cfg_.num_chars * H, &emb_);
+  put(hw[wi++], (size_t)cfg_.num_chars * emb_ch_, &emb_);
   if (cfg_.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {
     for (int l = 0; l < 3; ++l) {
       put_conv(pre_conv_[l], {{hw[wi], hw[wi + 1]}}, H, H, 5);
@@ -314,8 +319,11 @@ void GlowEncoder::reserve(int B, int T) {
 }
 
 void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m,
-                          float* x_logs, float* logw, float* x_mask, hipStream_t s, Profiler* prof, float* x_out) {
+                          float* x_logs, float* logw, float* x_mask, hipStream_t s, Profiler* prof, float* x_out,
+                          const float* lang) {
   TTS_REQUIRE(tok && len && x_m && x_mask && (logw || !with_dp_), 1, "NULL input/output pointer");
+  TTS_REQUIRE(emb_ch_ == cfg_.hidden_channels || lang != nullptr, 1,
+              "this encoder appends a language embedding (language_emb_dim > 0): pass lang_emb");
   TTS_REQUIRE(cfg_.c_in_channels == 0 || g != nullptr, 1, "c_in_channels > 0 requires g");
   TTS_REQUIRE(B >= 1 && T >= 1, 1, "batch and token count must be >= 1");
   // the attention kernel keeps whole score rows in LDS; the convolutional encoder types have no such bound
@@ -359,10 +367,11 @@ void GlowEncoder::forward(const int64_t* tok, const int64_t* len, const float* g
   // (normalization.py:42-53), the same normalisation with another eps
   const float eps_tf = cfg_.layer_norm_type == 2 ? 1e-5f : kEps;
 
-  // emb(x) * sqrt(H), transpose, x_mask (encoder.py:162-164)
-  const float scale = (float)std::sqrt((double)H);
+  // emb(x) * sqrt(H), transpose, x_mask (encoder.py:162-164); VITS with a language embedding:
+  // cat(emb(x) * sqrt(H), lang_emb.expand) with H the embedding width (vits/networks.py:86-96)
+  const float scale = (float)std::sqrt((double)emb_ch_);
   run(prof, s, "enc_embed", 0.0, 4.0 * P * H + 16.0 * P,
-      [&] { launch_embed(tok, len, emb_, X0, x_mask, B, H, T, cfg_.num_chars, scale, s); });
+      [&] { launch_embed(tok, len, emb_, X0, x_mask, B, H, T, cfg_.num_chars, scale, s, lang, emb_ch_); });
   float* x = X0;
   const int et = cfg_.encoder_type;
   if (cfg_.use_prenet && (et == TTS_ENC_REL_POS_TRANSFORMER || et == TTS_ENC_TIME_DEPTH_SEPARABLE)) {  // glow.py:61-67

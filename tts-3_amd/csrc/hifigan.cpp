@@ -358,7 +358,11 @@ int64_t Hifigan::plane_floats(int B, int T, int pad) const {
 // max-abs slot groups (fp16 hi/lo mode), [B][64] each: 0 the mel, 1 conv_pre's output, then per
 // stage i from stage_group(i): the upsampled input o, per resblock conv its output
 // (convs1 -> t, convs2 -> x), and the stage's MRF output z/num_kernels
-int Hifigan::n_planes() const { return 2 + 2 * nbs_; }
+int Hifigan::n_planes(int nbs) const { return 2 + 2 * nbs; }
+
+// branch streams of each lane when the batch splits over lanes: one, unless TTS_MI355X_MRF_STREAMS
+// asks for more (forward(); ADVICE r5: a split lane's region is sized for the planes it uses)
+int Hifigan::split_nbs() const { return nbs_env_ ? nbs_ : 1; }
 
 void Hifigan::ensure_lanes() {
   if (!lanes_.empty()) return;
@@ -385,10 +389,10 @@ void Hifigan::ensure_lanes() {
   ev_start_ = event();
 }
 
-int64_t Hifigan::lane_bytes(int B, int64_t L) const {
+int64_t Hifigan::lane_bytes(int B, int64_t L, int nbs) const {
   const int64_t cond = cond_floats(B);
   const int64_t amax = cfg_.math_mode == MATH_FP32_F16X3 ? (int64_t)amax_groups() * B * 64 : 0;
-  return ((n_planes() * plane_floats(B, (int)L, 0) + cond + amax + 63) / 64 * 64) * (int64_t)sizeof(float);
+  return ((n_planes(nbs) * plane_floats(B, (int)L, 0) + cond + amax + 63) / 64 * 64) * (int64_t)sizeof(float);
 }
 
 int Hifigan::amax_groups() const { return 2 + cfg_.num_upsamples * (2 + cfg_.num_kernels * 6); }
@@ -454,11 +458,15 @@ bool Hifigan::windowed(int64_t L) const {
   return L > max_window_frames() || (e && std::atoll(e) > 0 && L > std::atoll(e));
 }
 
-int64_t Hifigan::plain_workspace_bytes(int B, int64_t L) const {
-  // one region for the whole batch (profiled and windowed forwards), or one per lane
+int64_t Hifigan::plain_workspace_bytes(int B, int64_t L, bool window) const {
+  // the schedules forward() runs on this region: the whole batch as one lane with nbs_ branch
+  // streams (a window, B = 1 or one lane), one stream when profiled, or one region per lane of a
+  // split batch with split_nbs() streams each
+  const int nl = std::min(n_lanes_, B);
+  if (window || nl == 1) return lane_bytes(B, L, nbs_);
   int64_t lanes = 0;
-  for (int i = 0; i < n_lanes_; ++i) lanes += lane_bytes(lane_batch(B, i), L);
-  return std::max(lane_bytes(B, L), lanes);
+  for (int i = 0; i < nl; ++i) lanes += lane_bytes(lane_batch(B, i), L, split_nbs());
+  return std::max(lane_bytes(B, L, 1), lanes);
 }
 
 int64_t Hifigan::window_buffer_bytes(int B, int64_t W) const {
@@ -467,13 +475,13 @@ int64_t Hifigan::window_buffer_bytes(int B, int64_t W) const {
 
 int64_t Hifigan::workspace_bytes(int B, int T, int pad) const {
   const int64_t L = (int64_t)T + 2 * pad;
-  if (!windowed(L)) return plain_workspace_bytes(B, L);
+  if (!windowed(L)) return plain_workspace_bytes(B, L, false);
   const int64_t W = std::min<int64_t>(L, window_payload() + 2 * window_halo());
-  return plain_workspace_bytes(B, W) + window_buffer_bytes(B, W);
+  return plain_workspace_bytes(B, W, true) + window_buffer_bytes(B, W);
 }
 
-void Hifigan::reserve_plain(int B, int64_t L) {
-  const int64_t need = plain_workspace_bytes(B, L);
+void Hifigan::reserve_plain(int B, int64_t L, bool window) {
+  const int64_t need = plain_workspace_bytes(B, L, window);
   if ((size_t)need <= ws_bytes_) return;
   DeviceGuard g(device_);
   if (ws_) { TTS_HIP_CHECK(hipFree(ws_)); ws_ = nullptr; ws_bytes_ = 0; }
@@ -488,7 +496,7 @@ void Hifigan::reserve(int B, int T, int pad) {
     return;
   }
   const int64_t W = std::min<int64_t>(L, window_payload() + 2 * window_halo());
-  reserve_plain(B, W);
+  reserve_plain(B, W, true);
   const int64_t need = window_buffer_bytes(B, W);
   if ((size_t)need <= win_bytes_) return;
   DeviceGuard g(device_);
@@ -518,7 +526,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
     ensure_lanes();
     const int nl = std::min(n_lanes_, B);
     // split batches run one stream per lane unless TTS_MI355X_MRF_STREAMS says otherwise
-    for (Lane& ln : lanes_) ln.nbs = (nl > 1 && !nbs_env_) ? 1 : nbs_;
+    for (Lane& ln : lanes_) ln.nbs = nl > 1 ? split_nbs() : nbs_;
     if (nl == 1) {
       forward_plain(mel, B, C, T, pad, gvec, wav, s, nullptr, ws_, &lanes_[0]);
       return;
@@ -540,7 +548,7 @@ void Hifigan::forward(const float* mel, int B, int C, int T, int pad, const floa
         TTS_HIP_CHECK(hipEventRecord(ln.ev_done, si));
         TTS_HIP_CHECK(hipStreamWaitEvent(s, ln.ev_done, 0));
       }
-      ws += lane_bytes(Bi, L) / (int64_t)sizeof(float);
+      ws += lane_bytes(Bi, L, ln.nbs) / (int64_t)sizeof(float);
       b0 += Bi;
     }
     return;
@@ -579,7 +587,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
   const int64_t plane = plane_floats(B, T, pad);
   float* bufZ = ws;               // conv_pre output, then the MRF sum of each stage
   float* bufO = ws + plane;       // upsampled stage input o
-  const int np = n_planes();
+  const int np = n_planes(lane ? lane->nbs : 1);  // the planes this schedule uses (lane_bytes)
   float* cvec = cfg_.cond_channels > 0 ? ws + np * plane : nullptr;
   const bool h3 = cfg_.math_mode == MATH_FP32_F16X3;
   unsigned* amax = h3 ? reinterpret_cast<unsigned*>(ws + np * plane + cond_floats(B)) : nullptr;

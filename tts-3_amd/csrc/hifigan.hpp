@@ -121,17 +121,18 @@ class Hifigan {
   void forward_plain(const float* mel, int B, int C, int T, int pad, const float* g, float* wav, hipStream_t s,
                      Profiler* prof, float* ws, Lane* lane);
   void ensure_lanes();
-  int64_t lane_bytes(int B, int64_t L) const;
+  int64_t lane_bytes(int B, int64_t L, int nbs) const;
   int lane_batch(int B, int i) const { return B / n_lanes_ + (i < B % n_lanes_ ? 1 : 0); }
   bool windowed(int64_t L) const;
-  int64_t plain_workspace_bytes(int B, int64_t L) const;
+  int64_t plain_workspace_bytes(int B, int64_t L, bool window) const;
   int64_t window_buffer_bytes(int B, int64_t W) const;
-  void reserve_plain(int B, int64_t L);
+  void reserve_plain(int B, int64_t L, bool window = false);
   int64_t plane_floats(int B, int T, int pad) const;
   int64_t cond_floats(int B) const;
   int amax_groups() const;
   int stage_group(int i) const;
-  int n_planes() const;  // activation planes of a lane's workspace (Z, O, then X / T per branch stream)
+  int n_planes(int nbs) const;  // activation planes of a lane's workspace (Z, O, then X / T per branch stream)
+  int split_nbs() const;
 
   TtsHifiganCfg cfg_;
   int device_;

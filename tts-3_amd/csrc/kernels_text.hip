@@ -20,9 +20,9 @@ namespace tts {
 // x[b][c][t] = emb[tok[b][t]][c] * scale * mask[b][t];  mask[b][t] = t < len[b]
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) embed_kernel(const int64_t* __restrict__ tok, const int64_t* __restrict__ len,
-                                                    const float* __restrict__ emb, float* __restrict__ x,
-                                                    float* __restrict__ mask, int H, int T, int num_chars,
-                                                    float scale) {
+                                                    const float* __restrict__ emb, const float* __restrict__ lang,
+                                                    float* __restrict__ x, float* __restrict__ mask, int He, int H,
+                                                    int T, int num_chars, float scale) {
   const int b = blockIdx.y;
   const int t = blockIdx.x * 64 + (threadIdx.x & 63);
   const int cq = threadIdx.x >> 6;  // 4 waves split the channels
@@ -33,16 +33,21 @@ __global__ void __launch_bounds__(256) embed_kernel(const int64_t* __restrict__ 
   // the reference raises IndexError on an out-of-range id; padded positions carry any id
   // (they are masked), so clamp instead of reading out of bounds
   id = id < 0 ? 0 : (id >= num_chars ? num_chars - 1 : id);
-  const float* e = emb + (size_t)id * H;
+  const float* e = emb + (size_t)id * He;
   float* xo = x + (size_t)b * H * T + t;
-  for (int c = cq; c < H; c += 4) xo[(size_t)c * T] = e[c] * scale * m;
+  for (int c = cq; c < He; c += 4) xo[(size_t)c * T] = e[c] * scale * m;
+  // channels He .. H: the utterance's language embedding, cat((emb * sqrt(He), lang_emb.expand(T)))
+  // (vits/networks.py:90-91), masked with the rest (:96)
+  for (int c = He + cq; c < H; c += 4) xo[(size_t)c * T] = lang[(size_t)b * (H - He) + (c - He)] * m;
   if (cq == 0 && mask) mask[(size_t)b * T + t] = m;
 }
 
 void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, float* x, float* mask, int B, int H,
-                  int T, int num_chars, float scale, hipStream_t s) {
+                  int T, int num_chars, float scale, hipStream_t s, const float* lang, int He) {
+  if (He <= 0) He = H;
+  TTS_REQUIRE(He <= H && (He == H || lang != nullptr), 1, "embed: the language embedding channels need lang_emb");
   dim3 grid(ceil_div(T, 64), B);
-  hipLaunchKernelGGL(embed_kernel, grid, dim3(256), 0, s, tok, len, emb, x, mask, H, T, num_chars, scale);
+  hipLaunchKernelGGL(embed_kernel, grid, dim3(256), 0, s, tok, len, emb, lang, x, mask, He, H, T, num_chars, scale);
   TTS_HIP_CHECK(hipGetLastError());
 }
 

@@ -16,8 +16,10 @@ namespace tts {
 constexpr int ATTN_MAX_T = 3072;     // tokens per utterance (score rows live in LDS)
 constexpr int EXPAND_MAX_TX = 16384;  // tokens per utterance of the alignment expansion (LDS cumsum)
 
+// x [B][H][T] = cat(emb[tok] * scale (He channels), lang [B][H - He] broadcast over T) * mask
+// (He = 0: H, no language embedding)
 void launch_embed(const int64_t* tok, const int64_t* len, const float* emb, float* x, float* mask, int B, int H,
-                  int T, int num_chars, float scale, hipStream_t s);
+                  int T, int num_chars, float scale, hipStream_t s, const float* lang = nullptr, int He = 0);
 // y = LN_C(a [+ r]) * gamma + beta [relu] * mask (mask may be NULL); y may alias a or r
 void launch_layernorm(const float* a, const float* r, const float* gamma, const float* beta, const float* mask,
                       float* y, int B, int C, int T, float eps, bool relu, hipStream_t s);
@@ -77,23 +79,41 @@ void launch_sdp_affine(float* z, const float* tr, const float* ls, const float* 
                        hipStream_t s);
 void launch_sdp_spline(const float* h, float* z, const float* mask, int B, int T, int p, int nb, float tail,
                        float hscale, hipStream_t s);
+// Vits.inference glue (kernels_vits_text.hip)
+void launch_given_durations(const float* dur, int64_t dur_bstride, float* w_ceil, int64_t* y_len, int B, int T,
+                            hipStream_t s);
+void launch_mask_slice(const float* z, const float* m, float* out, int B, int C, int T, int T_out, hipStream_t s);
+void launch_upsample_z(const float* z, const int64_t* y_len, float* z2, float* m2, int B, int C, int T, int T2,
+                       double factor, hipStream_t s);
+void launch_embedding_rows(const float* table, const int64_t* ids, int64_t id_stride, float* out, int B, int dim,
+                           int num, hipStream_t s);
+void launch_l2_normalize(const float* d, float* out, int B, int C, hipStream_t s);
+void launch_add_vec_mask(const float* x, const float* v1, const float* v2, const float* m, float* y, int B, int C,
+                         int T, hipStream_t s);
+void launch_vec_add(const float* a, const float* b, float* out, int n, hipStream_t s);
 
-std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp = true);
+// emb_channels: width of emb.weight (0 = hidden_channels); less than hidden_channels for the VITS
+// TextEncoder with a language embedding, whose transformer runs at hidden + language_emb_dim
+std::vector<int64_t> glow_encoder_weight_shapes(const TtsGlowEncoderCfg& c, bool with_dp = true, int emb_channels = 0);
 void glow_encoder_validate(const TtsGlowEncoderCfg& c);
 
 class GlowEncoder {
  public:
   // with_dp = false: no duration predictor (its weights are absent from host_weights), the VITS
   // TextEncoder's use of the same RelativePositionTransformer (vits/networks.py:29-100)
-  GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* host_weights, int device, bool with_dp = true);
+  // emb_channels: see glow_encoder_weight_shapes (the embedding is scaled by sqrt(emb_channels))
+  GlowEncoder(const TtsGlowEncoderCfg& cfg, const float* const* host_weights, int device, bool with_dp = true,
+              int emb_channels = 0);
   ~GlowEncoder();
   GlowEncoder(const GlowEncoder&) = delete;
   GlowEncoder& operator=(const GlowEncoder&) = delete;
   // g: [B][c_in_channels] speaker vector (the reference's g [B][c_in][1]), NULL when c_in_channels == 0
   // x_out [B][H][T] (may be NULL): the encoder state before the heads (x * x_mask); logw may be NULL
   // without a duration predictor
+  // lang [B][hidden - emb_channels]: the language embedding appended to every token's embedding
   void forward(const int64_t* tok, const int64_t* len, const float* g, int B, int T, float* x_m, float* x_logs,
-               float* logw, float* x_mask, hipStream_t s, Profiler* prof = nullptr, float* x_out = nullptr);
+               float* logw, float* x_mask, hipStream_t s, Profiler* prof = nullptr, float* x_out = nullptr,
+               const float* lang = nullptr);
   int device() const { return device_; }
 
  private:
@@ -131,6 +151,7 @@ class GlowEncoder {
   TtsGlowEncoderCfg cfg_;
   int device_;
   bool with_dp_ = true;
+  int emb_ch_ = 0;
   float* emb_ = nullptr;
   Conv pre_conv_[3], pre_proj_;
   Norm pre_norm_[3];
@@ -158,8 +179,9 @@ TtsGlowEncoderCfg vits_text_encoder_glow_cfg(const TtsVitsTextEncoderCfg& c);
 class VitsTextEncoder {
  public:
   VitsTextEncoder(const TtsVitsTextEncoderCfg& cfg, const float* const* host_weights, int device);
-  void forward(const int64_t* tok, const int64_t* len, int B, int T, float* x, float* m, float* logs, float* x_mask,
-               hipStream_t s, Profiler* prof = nullptr);
+  // lang [B][language_emb_dim] (NULL without a language embedding); x [B][hidden + language_emb_dim][T]
+  void forward(const int64_t* tok, const int64_t* len, const float* lang, int B, int T, float* x, float* m,
+               float* logs, float* x_mask, hipStream_t s, Profiler* prof = nullptr);
   int device() const { return enc_->device(); }
 
  private:
@@ -178,8 +200,9 @@ class VitsSdp {
   VitsSdp& operator=(const VitsSdp&) = delete;
   // logw [B][1][T] = StochasticDurationPredictor(x, x_mask, g, reverse=True, noise_scale) with the
   // standard normal draw noise [B][2][T] given (stochastic_duration_predictor.py:256-282)
-  void reverse(const float* x, const float* x_mask, const float* g, const float* noise, float noise_scale, int B,
-               int T, float* logw, hipStream_t s, Profiler* prof = nullptr);
+  // lang [B][language_emb_dim] or NULL (cond_lang, :253-254)
+  void reverse(const float* x, const float* x_mask, const float* g, const float* lang, const float* noise,
+               float noise_scale, int B, int T, float* logw, hipStream_t s, Profiler* prof = nullptr);
   int device() const { return device_; }
 
  private:
@@ -212,6 +235,42 @@ class VitsSdp {
   std::vector<ConvFlow> flows_;  // flows.1 .. flows.num_flows
   float* cond_w_ = nullptr;      // cond [H][gin], bias [H] (fp32, launch_cond_vec)
   float* cond_b_ = nullptr;
+  float* lang_w_ = nullptr;      // cond_lang [H][L], bias [H]
+  float* lang_b_ = nullptr;
+  float* arena_ = nullptr;
+  float* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+};
+
+// The deterministic DurationPredictor of VITS with use_sdp=False (vits.py:694-702,
+// glow_tts/duration_predictor.py): x = x + cond(g) + cond_lang(lang); [2 x (conv k -> relu -> LayerNorm
+// (eps 1e-4))] -> proj (1x1) -> * mask
+std::vector<int64_t> vits_dp_weight_shapes(const TtsVitsDpCfg& c);
+void vits_dp_validate(const TtsVitsDpCfg& c);
+
+class VitsDp {
+ public:
+  VitsDp(const TtsVitsDpCfg& cfg, const float* const* host_weights, int device);
+  ~VitsDp();
+  VitsDp(const VitsDp&) = delete;
+  VitsDp& operator=(const VitsDp&) = delete;
+  void forward(const float* x, const float* x_mask, const float* g, const float* lang, int B, int T, float* logw,
+               hipStream_t s, Profiler* prof = nullptr);
+  int device() const { return device_; }
+
+ private:
+  struct Conv {
+    int Cin = 0, Cout = 0, K = 1, tile = 0, n_chunks = 0;
+    float* w = nullptr;
+    float* b = nullptr;
+  };
+  void reserve(int B, int T);
+
+  TtsVitsDpCfg cfg_;
+  int device_;
+  Conv c1_, c2_, proj_;
+  float *n1g_ = nullptr, *n1b_ = nullptr, *n2g_ = nullptr, *n2b_ = nullptr;
+  float *cond_w_ = nullptr, *cond_b_ = nullptr, *lang_w_ = nullptr, *lang_b_ = nullptr;
   float* arena_ = nullptr;
   float* ws_ = nullptr;
   size_t ws_bytes_ = 0;

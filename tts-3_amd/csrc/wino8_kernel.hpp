@@ -347,7 +347,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
 #pragma unroll
-        for (int q = 0; q < NP; ++q) ar[PD][q] = bload4(ra, avoff, aoff(ck, v + PD) + (unsigned)q * 1024u);
+        for (int q = 0; q < NP; ++q)
+          ar[PD][q] = (WINO_ABLATE & 4) ? ar[0][q]
+                                        : bload4(ra, avoff, ((WINO_ABLATE & 64) ? 0u : aoff(ck, v + PD)) + (unsigned)q * 1024u);
         if (v + 1 < NV) read_b(tl, v + 1, bnext);
         // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed), two DMA instructions per step
         if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc && v < 3) dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);

@@ -32,7 +32,8 @@ namespace tts {
 
 #ifndef WINO_ABLATE
 #define WINO_ABLATE 0  // ablation builds (timing only, wrong results): 1 no x loads, 2 no transform jobs, 4 no A stream,
-                       // 8 no MFMA, 16 no epilogue, 32 no input DMA (wino8)
+                       // 8 no MFMA, 16 no epilogue, 32 no input DMA (wino8),
+                       // 64 every A load from step 0 of the block (L1/L2 hits; wino8)
 #endif
 
 

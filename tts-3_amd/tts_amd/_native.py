@@ -29,7 +29,7 @@ TTS_ERR_OOM = 4
 MATH_MODES = {"fp32": 0, "fp32x6": 1, "f16x3": 2, "bf16": 3}
 
 # the C-ABI revision these bindings were written for (tts_abi_version() in csrc/abi.cpp)
-ABI_VERSION = 114
+ABI_VERSION = 115
 
 
 def default_math_mode(fp32_faithful_only: bool = True) -> str:
@@ -180,6 +180,17 @@ class TtsVitsSdpCfg(Structure):
     ]
 
 
+class TtsVitsDpCfg(Structure):
+    _fields_ = [
+        ("in_channels", c_int),
+        ("hidden_channels", c_int),
+        ("kernel_size", c_int),
+        ("cond_channels", c_int),
+        ("language_emb_dim", c_int),
+        ("math_mode", c_int),
+    ]
+
+
 class TtsLaunchRecord(Structure):
     _fields_ = [("name", c_char * 48), ("flops", c_double), ("bytes", c_double), ("ms", c_float)]
 
@@ -297,11 +308,12 @@ SIGNATURES = {
     ),
     "tts_vits_text_encoder_destroy": (c_int, [c_void_p]),
     "tts_vits_text_encoder_forward": (
-        c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                c_void_p]
     ),
     "tts_vits_text_encoder_forward_profiled": (
         c_int,
-        [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_vits_sdp_num_weights": (c_int, [POINTER(TtsVitsSdpCfg)]),
@@ -309,11 +321,22 @@ SIGNATURES = {
     "tts_vits_sdp_create": (c_int, [POINTER(TtsVitsSdpCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
     "tts_vits_sdp_destroy": (c_int, [c_void_p]),
     "tts_vits_sdp_reverse": (
-        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_void_p]
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p,
+                c_void_p]
     ),
     "tts_vits_sdp_reverse_profiled": (
         c_int,
-        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_void_p,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_void_p, c_void_p,
+         POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
+    ),
+    "tts_vits_dp_num_weights": (c_int, [POINTER(TtsVitsDpCfg)]),
+    "tts_vits_dp_weight_numel": (c_int64, [POINTER(TtsVitsDpCfg), c_int]),
+    "tts_vits_dp_create": (c_int, [POINTER(TtsVitsDpCfg), POINTER(c_void_p), c_int, POINTER(c_void_p)]),
+    "tts_vits_dp_destroy": (c_int, [c_void_p]),
+    "tts_vits_dp_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "tts_vits_dp_forward_profiled": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
          POINTER(TtsLaunchRecord), c_int, POINTER(c_int)],
     ),
     "tts_vits_durations": (c_int, [c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
@@ -322,6 +345,13 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_int, c_int,
          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "tts_vits_durations_given": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "tts_vits_mask_slice": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "tts_vits_upsample_z": (
+        c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p]
+    ),
+    "tts_embedding_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "tts_l2_normalize_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "tts_op_conv1d": (
         c_int, [POINTER(TtsConv1dDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     ),

@@ -417,20 +417,25 @@ def vits_text_encoder_state_dict(
     num_layers: int = VITS_TEXT_ENCODER["num_layers"],
     kernel_size: int = VITS_TEXT_ENCODER["kernel_size"],
     seed: int = 7531,
+    language_emb_dim: int = 0,
     **_unused,
 ) -> "OrderedDict[str, torch.Tensor]":
     """State dict of a VITS ``TextEncoder`` (TTS/tts/layers/vits/networks.py:29-81): the
     RelativePositionTransformer keys of ``glow_encoder_state_dict`` (LayerNorm2, window 4) under
     ``encoder.``, then ``proj`` (H -> 2 out); the log-scale rows of ``proj`` are drawn small so
-    exp(logs) stays O(1)."""
+    exp(logs) stays O(1).  language_emb_dim L > 0: the transformer and proj at H + L, the token
+    embedding at H (networks.py:58-64)."""
     ep = dict(kernel_size=kernel_size, num_layers=num_layers, num_heads=num_heads,
               hidden_channels_ffn=hidden_channels_ffn, rel_attn_window_size=4, layer_norm_type="2")
-    g = glow_encoder_state_dict(num_chars=num_chars, out_channels=out_channels, hidden_channels=hidden_channels,
+    H = hidden_channels + language_emb_dim
+    g = glow_encoder_state_dict(num_chars=num_chars, out_channels=out_channels, hidden_channels=H,
                                 encoder_params=ep, mean_only=True, use_prenet=False, seed=seed)
     sd: "OrderedDict[str, torch.Tensor]" = OrderedDict(
         (k, v) for k, v in g.items() if k == "emb.weight" or k.startswith("encoder."))
     rng = np.random.default_rng(seed + 1)
-    H = hidden_channels
+    if language_emb_dim:
+        e = rng.standard_normal((num_chars, hidden_channels)) * hidden_channels**-0.5  # nn.init.normal_(0, H^-0.5)
+        sd["emb.weight"] = torch.from_numpy(e.astype(np.float32))
     w = rng.standard_normal((2 * out_channels, H, 1)) / np.sqrt(H)
     w[out_channels:] *= 0.3
     sd["proj.weight"] = torch.from_numpy(w.astype(np.float32))
@@ -446,6 +451,7 @@ def vits_sdp_state_dict(
     cond_channels: int = 0,
     seed: int = 9753,
     log_duration: float = 1.6,
+    language_emb_dim: int = 0,
     **_unused,
 ) -> "OrderedDict[str, torch.Tensor]":
     """State dict of a VITS ``StochasticDurationPredictor`` (stochastic_duration_predictor.py:
@@ -505,6 +511,49 @@ def vits_sdp_state_dict(
         conv_flow(f"post_flows.{f + 1}")
     if cond_channels:
         conv("cond", H, cond_channels, 1)
+    if language_emb_dim:  # cond_lang (:226-227)
+        conv("cond_lang", H, language_emb_dim, 1)
+    return sd
+
+
+def vits_dp_state_dict(
+    in_channels: int = 192,
+    hidden_channels: int = 256,
+    kernel_size: int = 3,
+    cond_channels: int = 0,
+    language_emb_dim: int = 0,
+    seed: int = 4711,
+    log_duration: float = 1.6,
+    **_unused,
+) -> "OrderedDict[str, torch.Tensor]":
+    """State dict of the deterministic ``DurationPredictor`` VITS builds with use_sdp=False
+    (TTS/tts/layers/glow_tts/duration_predictor.py:21-47; in = in_channels + language_emb_dim):
+    variance-preserving convs, LayerNorm gamma ~ 1 + 0.1 N, and a proj whose bias puts exp(logw) at a
+    few frames per token."""
+    rng = np.random.default_rng(seed)
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    I, F, k = in_channels + language_emb_dim, hidden_channels, kernel_size
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+
+    def conv(name, cout, cin, kk, scale=1.0, bias_std=0.02, bias_mean=0.0):
+        sd[f"{name}.weight"] = t(rng.standard_normal((cout, cin, kk)) * (scale / np.sqrt(cin * kk)))
+        sd[f"{name}.bias"] = t(bias_mean + rng.standard_normal((cout,)) * bias_std)
+
+    def norm(name):
+        sd[f"{name}.gamma"] = t((1.0 + 0.1 * rng.standard_normal(F)).reshape(1, F, 1))
+        sd[f"{name}.beta"] = t((0.1 * rng.standard_normal(F)).reshape(1, F, 1))
+
+    conv("conv_1", F, I, k)
+    norm("norm_1")
+    conv("conv_2", F, F, k)
+    norm("norm_2")
+    conv("proj", 1, F, 1, scale=0.3, bias_mean=log_duration)
+    if cond_channels:
+        conv("cond", I, cond_channels, 1, scale=0.5)
+    if language_emb_dim:
+        conv("cond_lang", I, language_emb_dim, 1, scale=0.5)
     return sd
 
 

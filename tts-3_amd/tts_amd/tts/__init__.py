@@ -5,8 +5,8 @@
 from .glow_decoder import Decoder
 from .glow_tts import Encoder, GlowTTS
 from .vits_flow import PosteriorEncoder, ResidualCouplingBlocks
-from .vits_text import StochasticDurationPredictor, TextEncoder, Vits
+from .vits_text import DurationPredictor, StochasticDurationPredictor, TextEncoder, Vits
 from .xtts_decoder import HifiDecoder
 
-__all__ = ["Decoder", "Encoder", "GlowTTS", "HifiDecoder", "PosteriorEncoder", "ResidualCouplingBlocks",
+__all__ = ["Decoder", "DurationPredictor", "Encoder", "GlowTTS", "HifiDecoder", "PosteriorEncoder", "ResidualCouplingBlocks",
            "StochasticDurationPredictor", "TextEncoder", "Vits"]
