@@ -16,8 +16,16 @@ typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned OOB_OFF = 0x80000000u;
 
+#ifndef ACT_ABLATE
+#define ACT_ABLATE 0  // timing ablation only (wrong results): every activation-plane descriptor (a range
+                      // other than the weights' 0xFFFFFFFF) is cut to its first 64 KiB, so plane loads
+                      // past it return 0 and stores are dropped without touching memory
+#endif
+__device__ __forceinline__ unsigned act_range(unsigned bytes) {
+  return (ACT_ABLATE && bytes != 0xFFFFFFFFu && bytes > 65536u) ? 65536u : bytes;
+}
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)act_range(bytes), 0x00020000);
 }
 __device__ __forceinline__ float bload(rsrc_t r, unsigned voff, unsigned soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
@@ -54,7 +62,7 @@ __device__ __forceinline__ void lds_dma_b128(const void* base, unsigned bytes, u
   // every operand is wave-uniform; readfirstlane puts them in SGPRs (the "s" constraint alone does not)
   const u32x4_t d = {(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
                      (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)),
-                     (unsigned)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000u};
+                     (unsigned)__builtin_amdgcn_readfirstlane((int)act_range(bytes)), 0x00020000u};
   const unsigned m =
       (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long)(__attribute__((address_space(3))) const void*)lds);
 #pragma clang diagnostic push

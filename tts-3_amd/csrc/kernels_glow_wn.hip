@@ -16,6 +16,8 @@
 // those of the unfused layer; in f16x3 the acts operand takes the fixed exponent of |acts| < 1
 // instead of its per-utterance max-abs exponent (the same whenever max |acts| >= 0.5, and bitwise
 // on the test inputs); bf16x6 differs in the last bit of ~10% of the outputs (not isolated).
+#include <cstdlib>
+
 #include "glow.hpp"
 #include "split_device.hpp"
 
@@ -48,9 +50,9 @@ constexpr int WN_XP = WN_COLS + 1;            // fp32 pitch of the xin tile rows
 #endif
 constexpr int WN_ACTS_EXP = -14;              // f16x3 exponent of acts: |acts| < 1 -> [0, 2^14)
 
-template <class S, int TMW>
+template <class S, int H_>
 struct WnCfg {
-  static constexpr int H = 64 * TMW;
+  static constexpr int H = H_;
   static constexpr int NG = H / 16;  // 16-channel groups of h and acts
   static constexpr int HWIN = NG * WN_XR * S::ROWB;
   static constexpr int XIN = 2 * H * WN_XP * 4;
@@ -142,15 +144,23 @@ __device__ __forceinline__ void wn_gemm_rt(f32x16 (&acc)[TMW], f32x4 (&ar)[WN_PD
   }
 }
 
-template <class S, int K, int TMW>
-__global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args) {
-  using C = WnCfg<S, TMW>;
+// NW waves per workgroup: 4 (one per SIMD, TMW = H / 64 row blocks each), or more with the same MFMA
+// work per SIMD: 12 for H = 192 (three per SIMD, one row block each), 8 for H = 128 (one block) and
+// H = 256 (two), so a SIMD's waves hide each other's load, LDS and barrier latency and the staging,
+// gate and tail loops spread over more threads.  A wave whose block is past a GEMM's row count
+// skips that GEMM (TMW = 1), instead of computing a dropped block
+template <class S, int K, int H_, int NW>
+__global__ __launch_bounds__(64 * NW) void glow_wn_layer_kernel(GlowWnLayerArgs args) {
+  constexpr int TMW = 2 * H_ / 32 / NW;  // row blocks per wave (phase 1: 2H rows)
+  constexpr int NT = 64 * NW;            // threads
+  static_assert(TMW * NW * 32 == 2 * H_, "row blocks per wave");
+  using C = WnCfg<S, H_>;
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
   constexpr int H = C::H;
   constexpr int NG = C::NG;
   __shared__ __attribute__((aligned(16))) unsigned char smem[C::LDS];
-  __shared__ float red[4];  // the end conv's per-tile max-abs
+  __shared__ float red[NW];  // the end conv's per-tile max-abs
   unsigned char* hwin = smem;                   // stage / phase 1: the h window (split pieces)
   float* xin = reinterpret_cast<float*>(smem);  // after phase 1: xin tile [2H][WN_XP] fp32
   unsigned char* acts = smem + C::U1;           // phase 2's B operand (split pieces)
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     acc[m] = f32x16{};
-    ra[m] = make_rsrc(a.w_in + (size_t)(w + 4 * m) * a.steps_in * (NP * 256), 0xFFFFFFFFu);
+    ra[m] = make_rsrc(a.w_in + (size_t)(w + NW * m) * a.steps_in * (NP * 256), 0xFFFFFFFFu);
   }
   if (WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
   {
@@ -198,18 +208,18 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
       return (u < units && ts >= 0 && ts < Th) ? (unsigned)(16 * g + 4 * q) * rowb + (unsigned)ts * 4u : OOB_OFF;
     };
     if (WN_STAGE_BATCH) {
-      constexpr int UPT = (NG * 4 * WN_XR + 255) / 256;
+      constexpr int UPT = (NG * 4 * WN_XR + NT - 1) / NT;
       float v[UPT][4];
       int lds[UPT];
 #pragma unroll
       for (int i = 0; i < UPT; ++i) {
-        const unsigned off = unit_off(tid + 256 * i, lds[i]);
+        const unsigned off = unit_off(tid + NT * i, lds[i]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[i][j] = (WN_ABLATE & 8) ? 0.f : bload(rh, off + (unsigned)j * rowb, 0u);
       }
 #pragma unroll
       for (int i = 0; i < UPT; ++i) {
-        if (tid + 256 * i < units) {
+        if (tid + NT * i < units) {
           if (H3) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[i][j] *= xscale;
@@ -218,7 +228,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
         }
       }
     } else {
-      for (int u = tid; u < units; u += 256) {
+      for (int u = tid; u < units; u += NT) {
         int lds;
         const unsigned off = unit_off(u, lds);
         float v[4];
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
     for (int m = 0; m < TMW; ++m) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = 32 * (w + 4 * m) + (r & 3) + 8 * (r >> 2) + 4 * half;
+        const int row = 32 * (w + NW * m) + (r & 3) + 8 * (r >> 2) + 4 * half;
         const float bv = bload(rbias, (unsigned)row * 4u, 0u) + bload(rcv, (unsigned)row * 4u, 0u);
         xin[row * WN_XP + l32] = acc[m][r] + bv;
       }
@@ -264,18 +274,19 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   const int nmb = (a.last ? H : 2 * H) / 32;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
-    const int mb = w + 4 * m;
+    const int mb = w + NW * m;
     acc[m] = f32x16{};
     on[m] = mb < nmb;
-    ra[m] = make_rsrc(a.w_rs + (size_t)(mb < a.rs_blocks ? mb : w) * a.steps_rs * (NP * 256), 0xFFFFFFFFu);
+    ra[m] = make_rsrc(a.w_rs + (size_t)(mb < a.rs_blocks ? mb : 0) * a.steps_rs * (NP * 256), 0xFFFFFFFFu);
   }
-  if (WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
+  const bool run2 = TMW > 1 || on[0];  // wave-uniform: this wave has a res_skip block
+  if (WN_EARLY_A && run2) wn_prefetch<S, TMW>(ar, ra, avoff);
   __syncthreads();
 
   // ---- gate: acts = tanh(xin[c]) * sigmoid(xin[H + c]) (glow_gate_kernel), 4 channels per unit
   {
     const float ascale = H3 ? ldexpf(1.f, -WN_ACTS_EXP) : 1.f;
-    for (int u = tid; u < (H / 4) * WN_COLS; u += 256) {
+    for (int u = tid; u < (H / 4) * WN_COLS; u += NT) {
       const int col = u & (WN_COLS - 1);
       const int cq = u / WN_COLS;
       float av[4];
@@ -308,7 +319,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
     mv = bload(rmask, tok ? (unsigned)t * 4u : OOB_OFF, 0u);
 #pragma unroll
     for (int m = 0; m < TMW; ++m) {
-      const int mb = w + 4 * m;
+      const int mb = w + NW * m;
       const bool hrow = !last && mb < H / 32;  // wave-uniform: a 32-row block is one side
       const int prow0 = (hrow || last ? 32 * mb : 32 * mb - H) + 4 * half;
       const unsigned voff = (tok && on[m]) ? ((unsigned)prow0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
@@ -323,8 +334,8 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   if (WN_EPI_EARLY) epi_loads();
 
   // ---- phase 2: res_skip
-  if (!WN_EARLY_A) wn_prefetch<S, TMW>(ar, ra, avoff);
-  if (!(WN_ABLATE & 16)) wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
+  if (!WN_EARLY_A && run2) wn_prefetch<S, TMW>(ar, ra, avoff);
+  if (!(WN_ABLATE & 16) && run2) wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
     const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
 #pragma unroll
     for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
@@ -342,7 +353,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   float vmax = 0.f;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
-    const int mb = w + 4 * m;
+    const int mb = w + NW * m;
     if (!on[m]) continue;
     const bool hrow = !last && mb < H / 32;
     const int prow0 = (hrow || last ? 32 * mb : 32 * mb - H) + 4 * half;
@@ -381,7 +392,9 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   }
   __syncthreads();  // the max, and every wave is done reading acts
   if (H3) {
-    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float m = red[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) m = fmaxf(m, red[i]);
     if (m > 0.f && m < INFINITY) {
       int E;
       (void)frexpf(m, &E);
@@ -392,7 +405,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     if (!on[m]) continue;
-    const int mb = w + 4 * m;  // skip rows 32 mb .. + 31: channel groups 2 mb, 2 mb + 1
+    const int mb = w + NW * m;  // skip rows 32 mb .. + 31: channel groups 2 mb, 2 mb + 1
 #pragma unroll
     for (int gs = 0; gs < 2; ++gs)
       store_xt8<S>(acts + ((2 * mb + gs) * WN_COLS + l32) * S::ROWB + 16 * half, so[m], 8 * gs, sin_);
@@ -400,14 +413,15 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   const int nmb3 = a.end_rows / 32;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
-    const int mb = w + 4 * m;
+    const int mb = w + NW * m;
     acc[m] = f32x16{};
     on[m] = mb < nmb3;
-    ra[m] = make_rsrc(a.w_end + (size_t)(mb < a.end_blocks ? mb : w) * a.end_steps * (NP * 256), 0xFFFFFFFFu);
+    ra[m] = make_rsrc(a.w_end + (size_t)(mb < a.end_blocks ? mb : 0) * a.end_steps * (NP * 256), 0xFFFFFFFFu);
   }
-  wn_prefetch<S, TMW>(ar, ra, avoff);
+  const bool run3 = TMW > 1 || on[0];
+  if (run3) wn_prefetch<S, TMW>(ar, ra, avoff);
   __syncthreads();
-  wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
+  if (run3) wn_gemm<S, TMW, 1, NG>(acc, ar, ra, avoff, [&](int g, int, f32x4* dst) {
     const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
 #pragma unroll
     for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
@@ -423,7 +437,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 #pragma unroll
     for (int m = 0; m < TMW; ++m) {
       if (!on[m]) continue;
-      const int row0 = 32 * (w + 4 * m) + 4 * half;
+      const int row0 = 32 * (w + NW * m) + 4 * half;
       const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -444,7 +458,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     if (!on[m]) continue;
-    const int row0 = 32 * (w + 4 * m) + 4 * half;
+    const int row0 = 32 * (w + NW * m) + 4 * half;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = (r & 3) + 8 * (r >> 2);
@@ -462,7 +476,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
       for (int g = 0; g < SP; ++g) Wm[o][g] = a.winv[o * SP + g];
     const int G = C2 / SP;
     float vx = 0.f;
-    for (int u = tid; u < G * WN_COLS; u += 256) {
+    for (int u = tid; u < G * WN_COLS; u += NT) {
       const int col = u & (WN_COLS - 1);
       const int i = u / WN_COLS;
       const int tc = t0 + col;
@@ -508,7 +522,9 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   __syncthreads();
   int e2 = 0;
   if (H3) {
-    const float mm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float mm = red[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) mm = fmaxf(mm, red[i]);
     if (mm > 0.f && mm < INFINITY) {
       int E;
       (void)frexpf(mm, &E);
@@ -517,7 +533,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   }
   {
     const float s2 = H3 ? ldexpf(1.f, -e2) : 1.f;
-    for (int u = tid; u < (hf / 4) * WN_COLS; u += 256) {
+    for (int u = tid; u < (hf / 4) * WN_COLS; u += NT) {
       const int col = u & (WN_COLS - 1);
       const int cq = u / WN_COLS;
       float v[4];
@@ -532,14 +548,15 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   const int nmbs = H / 32;
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
-    const int mb = w + 4 * m;
+    const int mb = w + NW * m;
     acc[m] = f32x16{};
     on[m] = mb < nmbs;
-    ra[m] = make_rsrc(a.w_start + (size_t)(mb < a.start_blocks ? mb : w) * a.start_steps * (NP * 256), 0xFFFFFFFFu);
+    ra[m] = make_rsrc(a.w_start + (size_t)(mb < a.start_blocks ? mb : 0) * a.start_steps * (NP * 256), 0xFFFFFFFFu);
   }
-  wn_prefetch<S, TMW>(ar, ra, avoff);
+  const bool run4 = TMW > 1 || on[0];
+  if (run4) wn_prefetch<S, TMW>(ar, ra, avoff);
   __syncthreads();
-  wn_gemm_rt<S, TMW>(acc, ar, ra, hf / 16, avoff, [&](int g, int, f32x4* dst) {
+  if (run4) wn_gemm_rt<S, TMW>(acc, ar, ra, hf / 16, avoff, [&](int g, int, f32x4* dst) {
     const unsigned char* p = acts + (g * WN_COLS + l32) * S::ROWB + 16 * half;
 #pragma unroll
     for (int q = 0; q < NP; ++q) dst[q] = *reinterpret_cast<const f32x4*>(p + 32 * q);
@@ -556,7 +573,7 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
 #pragma unroll
   for (int m = 0; m < TMW; ++m) {
     if (!on[m]) continue;
-    const int row0 = 32 * (w + 4 * m) + 4 * half;
+    const int row0 = 32 * (w + NW * m) + 4 * half;
     const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Th + (unsigned)t) * 4u : OOB_OFF;
     float vm = 0.f;
 #pragma unroll
@@ -572,19 +589,41 @@ __global__ __launch_bounds__(256) void glow_wn_layer_kernel(GlowWnLayerArgs args
   if (H3 && a.amax_hnext) publish_amax(a.amax_hnext, b, hmax);
 }
 
-template <class S, int TMW>
+template <class S, int H, int NW>
 void launch_wn_s(const GlowWnLayerArgs& a, int B, hipStream_t s) {
   const dim3 grid(ceil_div(a.Th, WN_COLS), B);
-  if (a.K == 3) hipLaunchKernelGGL((glow_wn_layer_kernel<S, 3, TMW>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((glow_wn_layer_kernel<S, 5, TMW>), grid, dim3(256), 0, s, a);
+  if (a.K == 3) hipLaunchKernelGGL((glow_wn_layer_kernel<S, 3, H, NW>), grid, dim3(64 * NW), 0, s, a);
+  else hipLaunchKernelGGL((glow_wn_layer_kernel<S, 5, H, NW>), grid, dim3(64 * NW), 0, s, a);
+}
+
+// more than one wave per SIMD (round 6): H = 192 (Glow-TTS LJSpeech, the VITS flows and posterior
+// encoder) 12 waves, H = 128 and 256 eight; TTS_MI355X_WN_WAVES=4 keeps the round-5 four-wave form
+// (Glow decoder [16, 80, 768], MI355X A/B: f16x3 1.75 -> 1.52 ms, bf16 1.28 -> 1.01 ms,
+// profiles/ab_r06_wn_waves.txt)
+bool wn_four_waves() {
+  static const bool four = [] {
+    const char* e = std::getenv("TTS_MI355X_WN_WAVES");
+    return e && std::atoi(e) == 4;
+  }();
+  return four;
 }
 
 template <class S>
 void launch_wn_h(const GlowWnLayerArgs& a, int B, hipStream_t s) {
+  const bool four = wn_four_waves();
   switch (a.H) {
-    case 128: launch_wn_s<S, 2>(a, B, s); break;
-    case 192: launch_wn_s<S, 3>(a, B, s); break;
-    default: launch_wn_s<S, 4>(a, B, s); break;
+    case 128:
+      if (four) launch_wn_s<S, 128, 4>(a, B, s);
+      else launch_wn_s<S, 128, 8>(a, B, s);
+      break;
+    case 192:
+      if (four) launch_wn_s<S, 192, 4>(a, B, s);
+      else launch_wn_s<S, 192, 12>(a, B, s);
+      break;
+    default:
+      if (four) launch_wn_s<S, 256, 4>(a, B, s);
+      else launch_wn_s<S, 256, 8>(a, B, s);
+      break;
   }
 }
 
