@@ -279,3 +279,32 @@ def test_sdp_widest_hidden_vs_oracle(cuda_device):
     out = sdp.to(cuda_device)(x.to(cuda_device), xm.to(cuda_device), reverse=True, noise_scale=1.0,
                               noise=noise.to(cuda_device))
     assert_close_fp32(out.cpu(), ref, "sdp hidden 512", max_abs_tol=1e-4)
+
+
+def test_vits_inference_upsampling_non_integer_factor(cuda_device):
+    """upsampling_z at a non-integer interpolate_factor (24 kHz audio from a 16 kHz encoder: 1.5) through
+    Vits.inference with given durations (an even T_y, so the reference's z * y_mask shapes agree), against
+    the fp64 chain; an odd T_y raises as the reference's broadcast does."""
+    meta, arr = VT[0][1], VT[0][2]
+    d = cuda_device
+    m = dict(meta, up_factor=1.5)
+    v = _vits(m, d, "fp32x6", "f16x3", "f16x3", arr=arr)
+    assert abs(v.interpolate_factor - 1.5) < 1e-12
+    B, T = arr["tokens"].shape
+    dur = torch.full((1, T), 2.0)
+    dur[0, 0] = 3.0  # two 3-frame tokens: T_y = 2 T + 2, even
+    dur[0, 1] = 3.0
+    noise_z = torch.randn(B, 192, 64, generator=torch.Generator().manual_seed(12))
+    aux = {"x_lengths": torch.from_numpy(arr["lengths"]).to(d), "durations": dur.to(d), "noise_z": noise_z.to(d)}
+    out = v.inference(torch.from_numpy(arr["tokens"]).to(d), aux)
+    T_y = int(dur.sum())
+    assert T_y % 2 == 0 and out["z"].shape[2] == int(T_y * 1.5)
+    wc = torch.ceil(dur).reshape(1, 1, T).expand(B, 1, T).contiguous()
+    ref = oracle_chain(m, arr, w_ceil=wc, noise_z=noise_z)
+    assert torch.equal(out["y_mask"].cpu(), ref["y_mask_up"])
+    assert_close_fp32(out["z"].cpu(), ref["z"], "upsampled z (x1.5)", max_abs_tol=1e-4)
+    assert_close_fp32(out["model_outputs"].cpu(), ref["wav"], "wav (upsampling x1.5)")
+    dur[0, 2] = 3.0  # odd T_y: floor(1.5 T_y) frames of z against ceil(1.5 T_y) of mask
+    aux["durations"] = dur.to(d)
+    with pytest.raises(RuntimeError, match="upsampling_z"):
+        v.inference(torch.from_numpy(arr["tokens"]).to(d), aux)

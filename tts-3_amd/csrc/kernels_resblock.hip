@@ -29,13 +29,16 @@ namespace tts {
 //   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
 //   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
 //   instead of 92 KB); the halo costs (K - 1) / 192 of the columns instead of (K - 1) / 256.
+//   GEO 2 (C = 64, round 6 A/B, TTS_MI355X_PAIR_GEO64=2): RP_W = 128, waves 2 x 2 of 32 x 64,
+//   double-buffered staging: 51 KB of LDS and <= 168 VGPRs, three workgroups (three waves per
+//   SIMD) per CU.
 
 constexpr int kPostK = 7;     // conv_post kernel (hifigan_generator.py:229-230)
 constexpr int kPostHalo = 3;  // its zero-padding halo per side
 
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
-  static constexpr int RP_W = GEO == 0 ? 256 : 192;
+  static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
   static constexpr int RP_BN = RP_W - 2 * LEAD;
   static constexpr int WN = GEO == 0 ? 4 : 2;
@@ -64,7 +67,7 @@ struct PairCfg {
 // C = 32 (16-bit-pair schemes): ask for 3 waves per SIMD (<= 168 VGPRs + AGPRs): the LDS already
 // allows three workgroups per CU, the unconstrained allocation (173) allowed two
 template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 32 && S::ROWB <= 80 ? 3 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))
 void resblock_pair_kernel(ResPairArgs pa) {
   using P = PairCfg<S, K, C, PD, GEO, ALLX, POST>;
   constexpr int RP_W = P::RP_W, RP_BN = P::RP_BN;
@@ -401,7 +404,9 @@ void resblock_pair_kernel(ResPairArgs pa) {
 namespace {
 template <class S, int K, int C, int GEO>
 void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
-  constexpr bool AX = C == 64;  // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32
+  // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32; GEO 2 double-buffers
+  // (the LDS of three workgroups per CU)
+  constexpr bool AX = C == 64 && GEO != 2;
   if (a.post_w) {
     using P = PairCfg<S, K, C, 2, GEO, AX, true>;
     static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
@@ -413,9 +418,18 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX>), grid, dim3(256), 0, s, a);
 }
 
+int pair_geo64() {
+  static const int g = [] {
+    const char* e = std::getenv("TTS_MI355X_PAIR_GEO64");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+  return g;
+}
+
 template <class S, int K>
 void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
   if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
+  else if (C == 64 && pair_geo64() == 2 && S::ROWB <= 80) launch_pair_t<S, K, 64, 2>(a, B, s);
   else if (C == 64) launch_pair_t<S, K, 64, 1>(a, B, s);
   else throw Error(3, "resblock pair: channels must be 32 or 64");
 }

@@ -61,9 +61,12 @@ struct Res3Cfg {
   static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
+#ifndef RB3_W64
+#define RB3_W64 2  // A/B build option: waves per SIMD requested for the 64-channel 128-column block
+#endif
 template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD>
 __global__ __launch_bounds__((Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>::NT))
-__attribute__((amdgpu_waves_per_eu(C == 32 || (C == 64 && GEO == 2) || GEO == 3 ? 2 : 1)))
+__attribute__((amdgpu_waves_per_eu(C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO == 3 ? 2 : 1))))
 void resblock3_kernel(ResBlock3Args a) {
   using P = Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>;
   static_assert(NCV == 6 || NCV == 2, "ResBlock1 (6 convs) or ResBlock2 (2 convs)");
