@@ -88,8 +88,8 @@ def parse():
     p.add_argument("--no-vits", action="store_true", help="skip the VITS waveform-path measurement")
     p.add_argument("--no-vits-tts", action="store_true", help="skip the VITS tokens -> waveform measurement")
     p.add_argument("--no-rb2", action="store_true", help="skip the ResBlock2 (YourTTS decoder) measurement")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r05.json"))
-    p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r05.json"),
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_hifigan_r06.json"))
+    p.add_argument("--mfma-json", default=os.path.join(REPO, "profiles", "mfma_busy_r06.json"),
                    help="counter-derived MFMA-busy fractions per family (scripts/mfma_from_pmc.py)")
     p.add_argument("--cpu-utts", type=int, default=0,
                    help="utterances of the bench batch the CPU baseline vocodes (0: the whole batch)")
@@ -883,7 +883,7 @@ def main():
     achieved = exec_flops / (avg_ms / 1e3) / 1e12
     total_flops = sum(r["flops"] for r in rows)
     traffic = None
-    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r05.json)
+    fwd_bytes = None  # PMC HBM bytes of one forward (profiles/traffic_hifigan_r06.json)
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
