@@ -38,6 +38,9 @@ __device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? 
 //   cols  (MFMA j) = output time t
 //   depth (MFMA k) = input channel ci, looped over the K taps
 // ---------------------------------------------------------------------------------------
+constexpr int kPlaneXB16 = 1;  // Conv1dArgs::planes bit: the input x is a bf16 plane
+constexpr int kPlaneYB16 = 2;  //                          y / z / res are bf16 planes
+
 struct Conv1dArgs {
   const float* x;     // [B][Cin][Tin]
   const float* w;     // packed: [Cout_pad/BM][n_chunks][K][CK][BM]
@@ -77,6 +80,10 @@ struct Conv1dArgs {
   // sigmoid half (rows [H, 2H)) (gate_row_order); y receives acts [B][H][Tout] =
   // tanh(x_in[c]) * sigmoid(x_in[H + c]); bias is in packed row order, cvec in the original one.
   int gate;
+  // MATH_BF16 only (the HiFiGAN executor's bf16 activation planes, conv_device.hpp PlaneT): bit 0
+  // (kPlaneXB16) x is bf16, bit 1 (kPlaneYB16) y / z / res are bf16; the pointers keep their float
+  // type and address 2-byte elements.  0: fp32 everywhere.  mask / cvec / bias stay fp32.
+  int planes;
 };
 
 constexpr int kSplitGateTile = 20;  // = tile 13 (128 x 128, G = 2, PD = 2) with the gate epilogue
@@ -126,6 +133,7 @@ struct ResBlock3Args {
   float zdiv;
   unsigned* amax_out;       // [B][64] statistics of the stored value, or nullptr
   int T;
+  int planes;               // 0, or kPlaneXB16 | kPlaneYB16: x and z are bf16 planes (MATH_BF16)
 };
 bool resblock3_supported(int mode, int C, int K, const int* dil);
 void launch_resblock3(int mode, const ResBlock3Args& a, int B, int C, int K, hipStream_t s);
@@ -165,6 +173,7 @@ struct PostArgs {
   float* y;        // [B][1][T]
   int Cin, T;
   float in_slope;
+  int z_b16;       // z is a bf16 plane (MATH_BF16 activation planes); y stays fp32
 };
 
 // Host-side launchers (kernels_conv.hip).

@@ -50,6 +50,61 @@ __device__ __forceinline__ float bload_x(rsrc_t r, unsigned voff, unsigned soff)
 __device__ __forceinline__ void bstore(rsrc_t r, float v, unsigned voff, unsigned soff) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)voff, (int)soff, TTS_ST_POL);
 }
+// Activation planes in HBM (Conv1dArgs::planes): fp32, or bf16 in the MATH_BF16 scheme (the MFMA
+// operands are bf16 there anyway; the plane then costs 2 B per element instead of 4).  ES: bytes
+// per element; ld / st take byte offsets like bload / bstore.  A bf16 store rounds to nearest even
+// (v_cvt_pk_bf16_f32), a load widens exactly.
+__device__ __forceinline__ unsigned short f32_to_bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (__bf16)v);
+}
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned b) { return __builtin_bit_cast(float, b << 16); }
+__device__ __forceinline__ float bf16_round(float v) { return bf16_bits_to_f32(f32_to_bf16_bits(v)); }
+template <bool B16>
+struct PlaneT {
+  static constexpr unsigned ES = 4u;
+  __device__ static __forceinline__ float ld(rsrc_t r, unsigned voff, unsigned soff) { return bload(r, voff, soff); }
+  __device__ static __forceinline__ void st(rsrc_t r, float v, unsigned voff, unsigned soff) { bstore(r, v, voff, soff); }
+  // the value a store followed by a load gives back
+  __device__ static __forceinline__ float rt(float v) { return v; }
+};
+template <>
+struct PlaneT<true> {
+  static constexpr unsigned ES = 2u;
+  __device__ static __forceinline__ float ld(rsrc_t r, unsigned voff, unsigned soff) {
+    return bf16_bits_to_f32((unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, (int)voff, (int)soff, 0));
+  }
+  __device__ static __forceinline__ void st(rsrc_t r, float v, unsigned voff, unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b16(f32_to_bf16_bits(v), r, (int)voff, (int)soff, TTS_ST_POL);
+  }
+  __device__ static __forceinline__ float rt(float v) { return bf16_round(v); }
+};
+// element e of a plane based at p (float* in the argument blocks, bf16 when B16)
+template <bool B16>
+__device__ __forceinline__ const void* plane_at(const float* p, size_t e) {
+  return reinterpret_cast<const char*>(p) + e * PlaneT<B16>::ES;
+}
+// 4 consecutive elements at byte offset voff (8-byte aligned for bf16, 16 for fp32)
+template <bool B16>
+__device__ __forceinline__ f32x4 pload4(rsrc_t r, unsigned voff, unsigned soff) {
+  if constexpr (B16) {
+    const u32x2_t w = __builtin_bit_cast(u32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+    return f32x4{bf16_bits_to_f32(w[0] & 0xffffu), bf16_bits_to_f32(w[0] >> 16), bf16_bits_to_f32(w[1] & 0xffffu),
+                 bf16_bits_to_f32(w[1] >> 16)};
+  } else {
+    return bload4(r, voff, soff);
+  }
+}
+template <bool B16>
+__device__ __forceinline__ void pstore4(rsrc_t r, f32x4 v, unsigned voff, unsigned soff) {
+  if constexpr (B16) {
+    const u32x2_t w = {(unsigned)f32_to_bf16_bits(v[0]) | ((unsigned)f32_to_bf16_bits(v[1]) << 16),
+                       (unsigned)f32_to_bf16_bits(v[2]) | ((unsigned)f32_to_bf16_bits(v[3]) << 16)};
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, w), r, (int)voff, (int)soff, TTS_ST_POL);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, (int)voff, (int)soff, TTS_ST_POL);
+  }
+}
+
 // LDS-DMA of 16 bytes per lane (buffer_load_dwordx4 ... lds: lane l's bytes land at lds + 16 l),
 // issued from inline asm.  With the builtin, the compiler's waitcnt pass makes every later LDS
 // access of the issuing wave wait (vmcnt) until the DMA has landed, whatever buffer it touches, so
@@ -133,19 +188,20 @@ __device__ __forceinline__ void publish_amax_block(unsigned* slots, int b, float
 
 // sbias: bias + cvec of rows sbase.. already staged in LDS by the caller (rows >= Cout hold 0,
 // the same sums the two range-checked loads give), else nullptr
-template <int TM, int TN, bool RES, int ZM, bool AMAX>
+template <int TM, int TN, bool RES, int ZM, bool AMAX, bool YB = false>
 __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b,
                                                    int tbase, int cobase, int lane, int tend,
                                                    const float* sbias, int sbase) {
+  using PY = PlaneT<YB>;  // res / z / y element type
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int Cout = a.Cout;
   const int Tout = a.Tout;
-  const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;  // bytes of one batch item
+  const unsigned plane = (unsigned)Cout * (unsigned)Tout * PY::ES;  // bytes of one batch item
   const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
-  const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
-  const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
-  const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
+  const rsrc_t rres = make_rsrc(RES ? plane_at<YB>(a.res, item) : a.bias, RES ? plane : 0u);
+  const rsrc_t rz = make_rsrc(ZM >= 2 ? plane_at<YB>(a.z, item) : a.bias, ZM >= 2 ? plane : 0u);
+  const rsrc_t rout = make_rsrc(plane_at<YB>(a.zmode == 0 ? a.y : a.z, item), plane);
   const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * (a.cvec_bstride ? a.cvec_bstride : (int64_t)Cout) : a.bias,
                                a.cvec ? (unsigned)Cout * 4u : 0u);
   const rsrc_t rmask = make_rsrc(a.mask ? a.mask + (size_t)b * Tout : a.bias, a.mask ? (unsigned)Tout * 4u : 0u);
@@ -154,7 +210,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
   const bool mask_res = RES && a.mask_res && has_mask;
   const float oslope = a.out_slope;
   const float zdiv = a.zdiv;
-  const unsigned rowb = (unsigned)Tout * 4u;
+  const unsigned rowb = (unsigned)Tout * PY::ES;
   float vmax = 0.f;  // AMAX: max |stored value|
   // per 32x32 block: gather every value this thread reads, then compute and store.  Every
   // range-checked offset is in the per-lane voffset (lane row cobase + m*32 + 4*half, column t;
@@ -174,7 +230,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
       // rows >= Cout land past the plane through the row term; columns >= min(Tout, tend) are
       // marked OOB
       const bool tok = t < Tout && t < tend;
-      const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
+      const unsigned voff = tok ? ((unsigned)row0 * (unsigned)Tout + (unsigned)t) * PY::ES : OOB_OFF;
       const float mv = has_mask ? bload(rmask, (tok ? (unsigned)t * 4u : OOB_OFF), 0u) : 1.f;
       const float mv2 = mask_res ? mv : 1.f;  // (res + v) * mask for the VITS coupling update
       unsigned vo[16];
@@ -182,8 +238,8 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         vo[r] = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-        if (RES) rv[r] = bload(rres, vo[r], 0u);
-        if (ZM >= 2) zv[r] = bload(rz, vo[r], 0u);
+        if (RES) rv[r] = PY::ld(rres, vo[r], 0u);
+        if (ZM >= 2) zv[r] = PY::ld(rz, vo[r], 0u);
       }
       float vm = 0.f;
 #pragma unroll
@@ -194,7 +250,7 @@ __device__ __forceinline__ void conv_epilogue_impl(const Conv1dArgs& a, const f3
         if (ZM == 2) v = zv[r] + v;
         if (ZM == 3) v = (zv[r] + v) / zdiv;
         if (AMAX) vm = fmaxf(vm, fabsf(v));  // rows >= Cout hold exact zeros
-        bstore(rout, v, vo[r], 0u);
+        PY::st(rout, v, vo[r], 0u);
       }
       if (AMAX && tok) vmax = fmaxf(vmax, vm);
     }
@@ -268,10 +324,11 @@ __device__ __forceinline__ void conv_epilogue_wn(const Conv1dArgs& args, const f
 // -> y[b][co][U*m + s - U/2].  For U = 8 a lane's registers r = 4i..4i+3 hold the phases
 // 4*half .. 4*half+3 of one channel, i.e. 4 consecutive samples.
 // sb / scv: bias and cvec of rows sbase.. staged in LDS by the caller (or nullptr)
-template <int TM, int TN, bool AMAX>
+template <int TM, int TN, bool AMAX, bool YB = false>
 __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16 (&acc)[TM][TN], int b, int tbase,
                                                int cobase, int lane, const float* sb = nullptr,
                                                const float* scv = nullptr, int sbase = 0) {
+  using PY = PlaneT<YB>;
   const int half = lane >> 5;
   const int l32 = lane & 31;
   const int U = a.ups;
@@ -279,8 +336,8 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
   const int Cr = a.Cout >> lgU;   // channels
   const int Tin = a.Tin;
   const int To = Tin << lgU;      // output samples
-  const unsigned plane = (unsigned)Cr * (unsigned)To * 4u;
-  const rsrc_t rout = make_rsrc(a.y + (size_t)b * Cr * To, plane);
+  const unsigned plane = (unsigned)Cr * (unsigned)To * PY::ES;
+  const rsrc_t rout = make_rsrc(plane_at<YB>(a.y, (size_t)b * Cr * To), plane);
   const rsrc_t rbias = make_rsrc(a.bias, (unsigned)a.Cout * 4u);
   // cvec: 0 records when absent, so every read returns 0 and (acc + bias) + 0 is exact
   const rsrc_t rcv = make_rsrc(a.cvec ? a.cvec + (size_t)b * Cr : a.bias, a.cvec ? (unsigned)Cr * 4u : 0u);
@@ -306,14 +363,14 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
           const int rho = cobase + m * 32 + 8 * i + 4 * half;
           const int co = rho >> 3;
           const int t0 = (mm << 3) + 4 * half - 4;
-          const unsigned off = (t0 >= 0 && t0 < To) ? ((unsigned)co * (unsigned)To + (unsigned)t0) * 4u : OOB_OFF;
+          const unsigned off = (t0 >= 0 && t0 < To) ? ((unsigned)co * (unsigned)To + (unsigned)t0) * PY::ES : OOB_OFF;
           f32x4 v;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             v[j] = (acc[m][n][4 * i + j] + bv[4 * i + j]) + cv[4 * i + j];
             if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v[j]));
           }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)off, 0, TTS_ST_POL);
+          pstore4<YB>(rout, v, off, 0u);
         }
         continue;
       }
@@ -328,19 +385,20 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
           const float v0 = (acc[m][n][r] + bv[r]) + cv[r];
           const float v1 = (acc[m][n][r + 1] + bv[r + 1]) + cv[r + 1];
           const unsigned rowoff = (unsigned)co * (unsigned)To;
-          if (t >= 0 && t + 1 < To) {
+          if (!YB && t >= 0 && t + 1 < To) {
             if (AMAX && co < Cr) vmax = fmaxf(vmax, fmaxf(fabsf(v0), fabsf(v1)));
             const f32x2 v = {v0, v1};
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rout, (int)((rowoff + (unsigned)t) * 4u), 0, TTS_ST_POL);
           } else {
-            const unsigned off0 = (t >= 0 && t < To) ? (rowoff + (unsigned)t) * 4u : OOB_OFF;
-            const unsigned off1 = (t + 1 >= 0 && t + 1 < To) ? (rowoff + (unsigned)t + 1u) * 4u : OOB_OFF;
+            // (bf16: the pair starts at an odd sample, 2-byte aligned: two 16-bit stores)
+            const unsigned off0 = (t >= 0 && t < To) ? (rowoff + (unsigned)t) * PY::ES : OOB_OFF;
+            const unsigned off1 = (t + 1 >= 0 && t + 1 < To) ? (rowoff + (unsigned)t + 1u) * PY::ES : OOB_OFF;
             if (AMAX && co < Cr) {
               if (off0 != OOB_OFF) vmax = fmaxf(vmax, fabsf(v0));
               if (off1 != OOB_OFF) vmax = fmaxf(vmax, fabsf(v1));
             }
-            bstore(rout, v0, off0, 0u);
-            bstore(rout, v1, off1, 0u);
+            PY::st(rout, v0, off0, 0u);
+            PY::st(rout, v1, off1, 0u);
           }
         }
         continue;
@@ -351,10 +409,10 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
         const int co = rho >> lgU;
         const int t = (mm << lgU) + (rho & (U - 1)) - (U >> 1);
         // rows >= Cout land past the plane (co >= Cr); samples outside [0, To) are marked OOB
-        const unsigned off = (t >= 0 && t < To) ? ((unsigned)co * (unsigned)To + (unsigned)t) * 4u : OOB_OFF;
+        const unsigned off = (t >= 0 && t < To) ? ((unsigned)co * (unsigned)To + (unsigned)t) * PY::ES : OOB_OFF;
         const float v = (acc[m][n][r] + bv[r]) + cv[r];
         if (AMAX && off != OOB_OFF && co < Cr) vmax = fmaxf(vmax, fabsf(v));
-        bstore(rout, v, off, 0u);
+        PY::st(rout, v, off, 0u);
       }
     }
   }
@@ -363,14 +421,14 @@ __device__ __forceinline__ void convT_epilogue(const Conv1dArgs& a, const f32x16
 
 // The per-element options are template parameters (one uniform dispatch per tile), so the
 // unrolled epilogue carries no per-element branches.
-template <int TM, int TN, bool AMAX = false>
+template <int TM, int TN, bool AMAX = false, bool YB = false>
 __device__ __forceinline__ void conv_epilogue(const Conv1dArgs& args, const f32x16 (&acc)[TM][TN], int b,
                                               int tbase, int cobase, int lane, int tend = 0x7fffffff,
                                               const float* sbias = nullptr, int sbase = 0) {
   // copy the argument block: a store through `out` could alias it in the compiler's view
   const Conv1dArgs a = args;
   const int zm = a.zmode <= 1 ? 0 : a.zmode;
-#define TTS_EPI(RES, ZM) conv_epilogue_impl<TM, TN, RES, ZM, AMAX>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase)
+#define TTS_EPI(RES, ZM) conv_epilogue_impl<TM, TN, RES, ZM, AMAX, YB>(a, acc, b, tbase, cobase, lane, tend, sbias, sbase)
   if (a.res) {
     if (zm == 0) TTS_EPI(true, 0);
     else if (zm == 2) TTS_EPI(true, 2);

@@ -113,6 +113,10 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
   const char* sb = std::getenv("TTS_MI355X_SUBBATCH");
   n_lanes_ = sb ? std::max(1, std::min(std::atoi(sb), 8)) : 2;
   rb2_geo64_ = resblock2_geo64(mode);
+  // bf16 planes: every MRF stage length is then a multiple of 8 (the Winograd DMA's 16-byte rows)
+  const char* bp = std::getenv("TTS_MI355X_BF16_PLANES");
+  planes16_ = mode == MATH_BF16 && !(bp && bp[0] == '0') && cfg_.num_upsamples >= 1 &&
+              cfg_.upsample_factors[0] % 8 == 0;
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
   auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
@@ -617,10 +621,12 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
     a.Cin = Ld.Cin; a.Cout = Ld.Cout; a.Tin = Tin; a.Tout = Tout;
     a.dil = Ld.dil; a.pad = Ld.pad; a.rep_pad = rep; a.n_chunks = Ld.n_chunks;
     a.in_slope = in_slope; a.out_slope = out_slope; a.zmode = zmode; a.zdiv = (float)cfg_.num_kernels;
+    a.planes = planes16_ ? (x == mel ? kPlaneYB16 : kPlaneXB16 | kPlaneYB16) : 0;
+    const double ex = (planes16_ && x != mel) ? 2.0 : 4.0, ey = planes16_ ? 2.0 : 4.0;  // bytes per element
     const double flops = 2.0 * B * Ld.Cout * (double)Ld.Cin * Ld.K * Tout;
-    double bytes = 4.0 * ((double)B * Ld.Cin * Tin + (double)Ld.Cout * Ld.Cin * Ld.K + (double)B * Ld.Cout * Tout);
-    if (res) bytes += 4.0 * B * Ld.Cout * (double)Tout;
-    if (zmode >= 2) bytes += 4.0 * B * Ld.Cout * (double)Tout;
+    double bytes = ex * B * Ld.Cin * Tin + 4.0 * Ld.Cout * Ld.Cin * Ld.K + ey * B * Ld.Cout * Tout;
+    if (res) bytes += ey * B * Ld.Cout * (double)Tout;
+    if (zmode >= 2) bytes += ey * B * Ld.Cout * (double)Tout;
     run(prof, st, Ld.name.c_str(), flops, bytes, [&] { launch_conv(Ld.mode, a, B, Ld.K, Ld.tile, st); });
   };
 
@@ -647,9 +653,11 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
     const unsigned* z_amax = slots(i == 0 ? 1 : stage_group(i - 1) + 1 + cfg_.num_kernels * 6);
     const int lout = len * U.U;
     const double uflops = 2.0 * B * U.Cout * (double)U.Cin * 2 * lout;
-    const double ubytes = 4.0 * ((double)B * U.Cin * len + (double)U.Cin * U.Cout * 2 * U.U + (double)B * U.Cout * lout);
+    const double es = planes16_ ? 2.0 : 4.0;
+    const double ubytes = es * ((double)B * U.Cin * len + (double)B * U.Cout * lout) + 4.0 * U.Cin * U.Cout * 2 * U.U;
     if (is_split_mode(U.mode)) {
       Conv1dArgs a{};
+      a.planes = planes16_ ? kPlaneXB16 | kPlaneYB16 : 0;
       a.x = cur; a.w = U.w; a.bias = U.b; a.y = bufO;
       a.Cin = U.Cin; a.Cout = U.U * U.Cout; a.Tin = len; a.Tout = len + 1;
       a.dil = 1; a.pad = 1; a.n_chunks = U.n_chunks;
@@ -689,6 +697,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         // the three iterations in one launch: o -> MRF z
         ResBlock3Args ra{};
         ra.x = bufO; ra.amax_in = slots(g0);
+        ra.planes = planes16_ ? kPlaneXB16 | kPlaneYB16 : 0;
         for (int c = 0; c < 6; ++c) { ra.w[c] = rb.convs[c].w; ra.bias[c] = rb.convs[c].b; ra.w_exp[c] = rb.convs[c].w_exp; }
         for (int m = 0; m < 3; ++m) ra.dil[m] = rb.convs[2 * m].dil;
         ra.z = bufZ; ra.zmode = zlast; ra.zdiv = (float)cfg_.num_kernels;
@@ -696,7 +705,8 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         ra.T = len;
         const ConvLayer& L1 = rb.convs[0];
         const double flops = 12.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
-        const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 6.0 * L1.Cout * L1.Cin * L1.K);
+        const double bytes = (planes16_ ? 2.0 : 4.0) * B * L1.Cout * len * (zlast >= 2 ? 3 : 2) +
+                             4.0 * 6.0 * L1.Cout * L1.Cin * L1.K;
         const std::string nm = "mrf_block_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
         zorder();
         run(prof, sj, nm.c_str(), flops, bytes, [&] { launch_resblock3(L1.mode, ra, B, L1.Cout, L1.K, sj); });
@@ -715,12 +725,14 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
           c1.x = xin; c1.w = L1.w; c1.bias = L1.b; c1.Cin = L1.Cin; c1.Cout = L1.Cout; c1.Tin = len; c1.Tout = len;
           c1.dil = L1.dil; c1.pad = L1.pad; c1.n_chunks = L1.n_chunks; c1.in_slope = 0.1f; c1.out_slope = 0.1f;
           c1.zdiv = 1.f; c1.w_exp = L1.w_exp;
+          c1.planes = planes16_ ? kPlaneXB16 | kPlaneYB16 : 0;
           c1.amax_in = (m == 0) ? slots(g0) : slots(gj + 2 * m - 1);
           Conv1dArgs& c2 = pa.c2;
           c2.x = nullptr; c2.w = L2.w; c2.bias = L2.b; c2.res = xin; c2.y = xout; c2.z = bufZ;
           c2.Cin = L2.Cin; c2.Cout = L2.Cout; c2.Tin = len; c2.Tout = len; c2.dil = 1; c2.pad = L2.pad;
           c2.n_chunks = L2.n_chunks; c2.in_slope = 1.f; c2.out_slope = 1.f; c2.zmode = last ? zlast : 0;
           c2.zdiv = (float)cfg_.num_kernels; c2.w_exp = L2.w_exp;
+          c2.planes = c1.planes;
           c2.amax_out = last ? (j == cfg_.num_kernels - 1 ? slots(gz) : nullptr) : slots(gj + 2 * m + 1);
           // the generator's last MRF writer: conv_post runs in its epilogue (the final z never
           // reaches HBM); TTS_MI355X_POST_FUSION=0 keeps the separate conv_post launch
@@ -732,11 +744,11 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
             post_done = true;
           }
           double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
-          double bytes = 4.0 * ((double)B * L1.Cout * len * (last ? (zlast >= 2 ? 4 : 3) : 3) +
-                                2.0 * L1.Cout * L1.Cin * L1.K);
+          const double es = planes16_ ? 2.0 : 4.0;
+          double bytes = es * B * L1.Cout * len * (last ? (zlast >= 2 ? 4 : 3) : 3) + 4.0 * 2.0 * L1.Cout * L1.Cin * L1.K;
           if (post) {
             flops += 2.0 * B * len * (double)L1.Cout * 7;
-            bytes += 4.0 * ((double)B * len - (double)B * L1.Cout * len);  // + wav, - the z store
+            bytes += 4.0 * B * len - es * B * L1.Cout * len;  // + wav, - the z store
           }
           const std::string nm = std::string(post ? "mrf_pair_post_k" : "mrf_pair_k") + std::to_string(L1.K) +
                                  "_c" + std::to_string(L1.Cout);
@@ -762,6 +774,7 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         // both convs in one launch: o -> MRF z
         ResBlock3Args ra{};
         ra.x = bufO; ra.amax_in = slots(g0);
+        ra.planes = planes16_ ? kPlaneXB16 | kPlaneYB16 : 0;
         for (int c = 0; c < 2; ++c) {
           ra.w[c] = rb.convs[c].w; ra.bias[c] = rb.convs[c].b; ra.w_exp[c] = rb.convs[c].w_exp;
           ra.dil[c] = rb.convs[c].dil;
@@ -771,7 +784,8 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
         ra.T = len;
         const ConvLayer& L1 = rb.convs[0];
         const double flops = 4.0 * B * L1.Cout * (double)L1.Cin * L1.K * len;
-        const double bytes = 4.0 * ((double)B * L1.Cout * len * (zlast >= 2 ? 3 : 2) + 2.0 * L1.Cout * L1.Cin * L1.K);
+        const double bytes = (planes16_ ? 2.0 : 4.0) * B * L1.Cout * len * (zlast >= 2 ? 3 : 2) +
+                             4.0 * 2.0 * L1.Cout * L1.Cin * L1.K;
         const std::string nm = "mrf_block2_k" + std::to_string(L1.K) + "_c" + std::to_string(L1.Cout);
         zorder();
         run(prof, sj, nm.c_str(), flops, bytes,
@@ -799,8 +813,9 @@ void Hifigan::forward_plain(const float* mel, int B, int C, int T, int pad, cons
   PostArgs pa{};
   pa.z = bufZ; pa.w = post_wd_; pa.bias = post_bias_; pa.y = wav;
   pa.Cin = C0 >> cfg_.num_upsamples; pa.T = len; pa.in_slope = 0.01f;
+  pa.z_b16 = planes16_ ? 1 : 0;
   run(prof, s, "conv_post", 2.0 * B * len * (double)pa.Cin * 7,
-      4.0 * ((double)B * pa.Cin * len + (double)B * len), [&] { launch_conv_post(pa, B, s); });
+      (planes16_ ? 2.0 : 4.0) * B * pa.Cin * len + 4.0 * B * len, [&] { launch_conv_post(pa, B, s); });
 }
 
 }  // namespace tts

@@ -139,6 +139,9 @@ class Hifigan {
   int hop_ = 1;
   int rb2_geo64_ = 0;         // ResBlock2 at 64 channels: 1 = 192-column tiles (resblock2_geo64)
   bool post_fusion_ = true;  // conv_post inside the last MRF launch (TTS_MI355X_POST_FUSION=0: off)
+  // MATH_BF16: the Z / O / X / T activation planes hold bf16 (conv_device.hpp PlaneT), halving the
+  // bytes every kernel stages, gathers and stores; TTS_MI355X_BF16_PLANES=0 keeps fp32 planes
+  bool planes16_ = false;
   // defaults (A/B on MI355X, config 2): two sub-batch lanes with one stream each when B >= 2
   // (51.5 ms per batch), else one lane with a stream per MRF branch (51.8 ms at B = 32; 3 x 2
   // streams: 52.5 ms)

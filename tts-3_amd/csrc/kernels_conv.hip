@@ -403,7 +403,10 @@ constexpr int POST_C = 8;
 constexpr int POST_W = POST_T + 8;
 constexpr int POST_MAXC = 64;
 
+// ZB: z is a bf16 plane (PostArgs::z_b16, the bf16 scheme's activation planes)
+template <bool ZB = false>
 __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
+  using PZ = PlaneT<ZB>;
   __shared__ __attribute__((aligned(16))) float zs[2][POST_C][POST_W];
   __shared__ float ws[POST_MAXC * POST_K];
   const int Cin = a.Cin;
@@ -411,8 +414,7 @@ __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
   const int tid = threadIdx.x;
   const int t0 = blockIdx.x * POST_T;
   const int b = blockIdx.y;
-  const float* zb = a.z + (size_t)b * Cin * T;
-  const rsrc_t rz = make_rsrc(zb, (unsigned)Cin * (unsigned)T * 4u);
+  const rsrc_t rz = make_rsrc(plane_at<ZB>(a.z, (size_t)b * Cin * T), (unsigned)Cin * (unsigned)T * PZ::ES);
   const float slope = a.in_slope;
   for (int e = tid; e < Cin * POST_K; e += 256) ws[e] = a.w[e];
   // per thread: 4 interior samples t0 + 4*tid + j, and for tid < 6 one halo sample
@@ -429,8 +431,8 @@ __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
       const unsigned row = (unsigned)ci * (unsigned)T;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        xi[c][j] = bload(rz, (ci < Cin && ti + j < T) ? (row + (unsigned)(ti + j)) * 4u : OOB_OFF, 0u);
-      xh[c] = bload(rz, (ci < Cin && hok) ? (row + (unsigned)th) * 4u : OOB_OFF, 0u);
+        xi[c][j] = PZ::ld(rz, (ci < Cin && ti + j < T) ? (row + (unsigned)(ti + j)) * PZ::ES : OOB_OFF, 0u);
+      xh[c] = PZ::ld(rz, (ci < Cin && hok) ? (row + (unsigned)th) * PZ::ES : OOB_OFF, 0u);
     }
   };
   auto store = [&](int buf) {
@@ -476,7 +478,9 @@ __global__ __launch_bounds__(256) void conv_post_kernel(PostArgs a) {
 // vector beyond their wave's edge themselves (out-of-range vectors read as the zero padding).
 // 8 channels of loads are in flight ahead of the math.  Same FMA order as conv_post_kernel.
 constexpr int POST4_C = 8;
+template <bool ZB = false>
 __global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
+  using PZ = PlaneT<ZB>;
   __shared__ float ws[POST_MAXC * POST_K];
   const int Cin = a.Cin;
   const int T = a.T;
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
   const int lane = tid & 63;
   const int b = blockIdx.y;
   const int ti = blockIdx.x * POST_T + 4 * tid;
-  const rsrc_t rz = make_rsrc(a.z + (size_t)b * Cin * T, (unsigned)Cin * (unsigned)T * 4u);
+  const rsrc_t rz = make_rsrc(plane_at<ZB>(a.z, (size_t)b * Cin * T), (unsigned)Cin * (unsigned)T * PZ::ES);
   const float slope = a.in_slope;
   for (int e = tid; e < Cin * POST_K; e += 256) ws[e] = a.w[e];
   const bool inb = ti < T;
@@ -497,8 +501,8 @@ __global__ __launch_bounds__(256) void conv_post4_kernel(PostArgs a) {
     for (int c = 0; c < POST4_C; ++c) {
       const int ci = cb * POST4_C + c;
       const unsigned row = (unsigned)ci * (unsigned)T;
-      m[c] = bload4(rz, (ci < Cin && inb) ? (row + (unsigned)ti) * 4u : OOB_OFF, 0u);
-      e[c] = bload4(rz, (ci < Cin && eok) ? (row + (unsigned)te) * 4u : OOB_OFF, 0u);
+      m[c] = pload4<ZB>(rz, (ci < Cin && inb) ? (row + (unsigned)ti) * PZ::ES : OOB_OFF, 0u);
+      e[c] = pload4<ZB>(rz, (ci < Cin && eok) ? (row + (unsigned)te) * PZ::ES : OOB_OFF, 0u);
     }
   };
   load(cm, ce, 0);
@@ -733,8 +737,13 @@ void launch_conv_post(const PostArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.T, POST_T), B);
   // the vector form needs 16-byte aligned rows (T % 4 == 0) and plane bases
   const bool vec = a.T % 4 == 0 && ((uintptr_t)a.z & 15) == 0 && ((uintptr_t)a.y & 15) == 0;
-  if (vec) hipLaunchKernelGGL(conv_post4_kernel, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(conv_post_kernel, grid, dim3(256), 0, s, a);
+  if (a.z_b16) {
+    if (vec) hipLaunchKernelGGL(conv_post4_kernel<true>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv_post_kernel<true>, grid, dim3(256), 0, s, a);
+  } else {
+    if (vec) hipLaunchKernelGGL(conv_post4_kernel<false>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv_post_kernel<false>, grid, dim3(256), 0, s, a);
+  }
   TTS_HIP_CHECK(hipGetLastError());
 }
 

@@ -21,6 +21,7 @@
 // tap 0 then tap 1, the scheme's products; f16x3 input scale from the producer's statistics).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "split_device.hpp"
 
@@ -56,8 +57,11 @@ struct ConvTResCfg {
 
 // RS: workgroups per window, each taking 1 / RS of the passes (restages the window RS times; the
 // 512-channel layer's 544 windows would fill the 256 CUs only 2.1 times over)
-template <class S, int NG, int WR, int TN_, int RS>
+// PL: Conv1dArgs::planes (the bf16 scheme: 0, or bf16 input and output planes)
+template <class S, int NG, int WR, int TN_, int RS, int PL = 0>
 __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
+  constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
+  using PX = PlaneT<XB>;
   using P = ConvTResCfg<S, NG, WR, TN_>;
   using R = ConvTResRow<S>;
   constexpr int RB = R::RB;
@@ -86,8 +90,8 @@ __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
 
   // ---- stage frames t0 - 1 .. t0 + BN of every channel (zero outside [0, Tin)) ----
   {
-    const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
-    const unsigned chb = (unsigned)Tin * 4u;
+    const void* xb = plane_at<XB>(a.x, (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin));
+    const unsigned chb = (unsigned)Tin * PX::ES;
     const rsrc_t rx = make_rsrc(xb, (unsigned)Cin * chb);
     f32x4 xr[P::UPT];
 #pragma unroll
@@ -99,9 +103,9 @@ __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
       const int ts = t0 - 1 + r;
       const bool ok = g < NG && ts >= 0 && ts < Tin;
       // OOB_OFF + 3 * chb stays out of range (planes < 2 GiB)
-      const unsigned vo = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+      const unsigned vo = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * PX::ES : OOB_OFF;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xr[i][j] = bload(rx, vo + (unsigned)j * chb, 0u);
+      for (int j = 0; j < 4; ++j) xr[i][j] = PX::ld(rx, vo + (unsigned)j * chb, 0u);
     }
 #pragma unroll
     for (int i = 0; i < P::UPT; ++i) {
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(512) void convT_res_kernel(Conv1dArgs a) {
 #pragma unroll
       for (int n = 0; n < TN; ++n) acc[0][n] *= sc;
     }
-    convT_epilogue<1, TN, H3>(a, acc, b, t0 + wc * TN * 32, (pass * WR + wr) * 32, lane);
+    convT_epilogue<1, TN, H3, YB>(a, acc, b, t0 + wc * TN * 32, (pass * WR + wr) * 32, lane);
   }
 }
 
@@ -212,6 +216,13 @@ void launch_res_t(const Conv1dArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.Cin == 16 * NG && a.Cout % (32 * WR) == 0 && a.Cout / (32 * WR) >= RS, 1,
               "convT_res: bad shape for this instance");
   const dim3 grid(ceil_div(a.Tout, ConvTResCfg<S, NG, WR, TN>::BN), B, RS);
+  if (a.planes != 0) {
+    constexpr bool OK = std::is_same<S, SchemeB1>::value;
+    TTS_REQUIRE(OK && a.planes == (kPlaneXB16 | kPlaneYB16), 3, "convT_res: bf16 planes need the bf16 scheme");
+    if constexpr (OK)
+      hipLaunchKernelGGL((convT_res_kernel<S, NG, WR, TN, RS, kPlaneXB16 | kPlaneYB16>), grid, dim3(512), 0, s, a);
+    return;
+  }
   hipLaunchKernelGGL((convT_res_kernel<S, NG, WR, TN, RS>), grid, dim3(512), 0, s, a);
 }
 // 256-row passes (8 row-block waves, 64-frame windows)

@@ -34,6 +34,9 @@ void launch_wino(int mode, const Conv1dArgs& a, int B, int K, hipStream_t s) {
               "conv1d: a batch item's channel plane exceeds 2 GiB");
   // the 8-wave form needs 16-byte aligned input rows (every HiFiGAN MRF conv at >= 128 channels:
   // T = 8 * (T_mel + 2 pad) and more); other lengths take the 4-wave form
+  // bf16 activation planes (Conv1dArgs::planes): the 8-wave form only, its DMA needs T % 8 == 0
+  TTS_REQUIRE(a.planes == 0 || (mode == MATH_BF16 && a.Tin % 8 == 0), 3,
+              "conv1d(winograd): bf16 planes need the bf16 scheme and T % 8 == 0");
   if (mode == MATH_BF16) {
     if (a.Tin % 4 == 0) wino8_detail::launch_s<SchemeB1>(a, B, K, s);
     else wino_detail::launch_wino_s<SchemeB1>(a, B, K, s);

@@ -15,6 +15,7 @@
 // The residual x is re-read from global memory, so x and x' must not alias (ping-pong buffers).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "resblock_block.hpp"
 #include "split_device.hpp"
@@ -66,9 +67,13 @@ struct PairCfg {
 
 // C = 32 (16-bit-pair schemes): ask for 3 waves per SIMD (<= 168 VGPRs + AGPRs): the LDS already
 // allows three workgroups per CU, the unconstrained allocation (173) allowed two
-template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false>
+// PL: the planes of x, x' / z (bf16 in the bf16 scheme's activation-plane form, Conv1dArgs::planes)
+template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false, int PL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))
 void resblock_pair_kernel(ResPairArgs pa) {
+  constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
+  using PX = PlaneT<XB>;
+  using PY = PlaneT<YB>;
   using P = PairCfg<S, K, C, PD, GEO, ALLX, POST>;
   constexpr int RP_W = P::RP_W, RP_BN = P::RP_BN;
   constexpr int NP = S::NP;
@@ -107,10 +112,10 @@ void resblock_pair_kernel(ResPairArgs pa) {
     const Conv1dArgs a2 = q.c2;
     const int hf = ln >> 5, lo = ln & 31;
     const size_t item = (size_t)bb * C * T;
-    const unsigned plane = (unsigned)C * (unsigned)T * 4u;
-    const rsrc_t rres = make_rsrc(a2.res + item, plane);
-    const rsrc_t rz = make_rsrc(a2.z + item, plane);
-    const unsigned rowb = (unsigned)T * 4u;
+    const unsigned plane = (unsigned)C * (unsigned)T * PY::ES;
+    const rsrc_t rres = make_rsrc(plane_at<YB>(a2.res, item), plane);
+    const rsrc_t rz = make_rsrc(plane_at<YB>(a2.z, item), plane);
+    const unsigned rowb = (unsigned)T * PY::ES;
     float* zt = reinterpret_cast<float*>(smem);
     __syncthreads();  // every wave is past its last phase-2 read of xt
 #pragma unroll
@@ -121,13 +126,13 @@ void resblock_pair_kernel(ResPairArgs pa) {
         const int t = tt0 + col;
         const bool tok = t >= 0 && t < T && col < RP_BN;
         const int rw0 = row0w + m * 32 + 4 * hf;
-        const unsigned voff = tok ? ((unsigned)rw0 * (unsigned)T + (unsigned)t) * 4u : OOB_OFF;
+        const unsigned voff = tok ? ((unsigned)rw0 * (unsigned)T + (unsigned)t) * PY::ES : OOB_OFF;
         float rv[16], zv[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const unsigned vo = voff + (unsigned)((r & 3) + 8 * (r >> 2)) * rowb;
-          rv[r] = bload(rres, vo, 0u);
-          zv[r] = bload(rz, vo, 0u);
+          rv[r] = PY::ld(rres, vo, 0u);
+          zv[r] = PY::ld(rz, vo, 0u);
         }
         if (col < RP_BN) {
 #pragma unroll
@@ -137,8 +142,9 @@ void resblock_pair_kernel(ResPairArgs pa) {
             v = lrelu2(v, a2.out_slope);
             v = (v + rv[r]) * 1.f;
             v = (zv[r] + v) / a2.zdiv;
-            // conv_post reads lrelu(z): applied once here instead of once per tap
-            zt[row * RP_BN + col] = tok ? lrelu(v, q.post_slope) : 0.f;
+            // conv_post reads lrelu(z): applied once here instead of once per tap (bf16 planes:
+            // on the value the stored plane would hold, so the separate conv_post gives the same)
+            zt[row * RP_BN + col] = tok ? lrelu(PY::rt(v), q.post_slope) : 0.f;
           }
         }
       }
@@ -161,8 +167,8 @@ void resblock_pair_kernel(ResPairArgs pa) {
   // ------------------------------------------------------------------ phase 1: convs1
   const int ex = H3 ? amax_exp(a1.amax_in, b) : 0;
   const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;
-  const float* xb = a1.x + (size_t)b * C * T;
-  const unsigned chb = (unsigned)T * 4u;
+  const char* xb = static_cast<const char*>(plane_at<XB>(a1.x, (size_t)b * C * T));
+  const unsigned chb = (unsigned)T * PX::ES;
   unsigned uvoff[P::UPT];
   int ulds[P::UPT];
 #pragma unroll
@@ -173,17 +179,17 @@ void resblock_pair_kernel(ResPairArgs pa) {
     const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
     const int ts = tx0 - a1.pad + r;
     const bool ok = r < XW && ts >= 0 && ts < T;
-    uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * 4u : OOB_OFF;
+    uvoff[i] = ok ? (unsigned)(4 * q) * chb + (unsigned)ts * PX::ES : OOB_OFF;
     ulds[i] = r < XW ? r * S::ROWB + 8 * quad_pos(q) : -1;
   }
   f32x4 xall[ALLX ? NC : 1][P::UPT];
   auto load_x = [&](int c) {
     f32x4 (&xreg)[P::UPT] = xall[ALLX ? c : 0];
-    const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * T, (unsigned)(C - c * 16) * chb);
+    const rsrc_t rx = make_rsrc(xb + (size_t)c * 16 * chb, (unsigned)(C - c * 16) * chb);
 #pragma unroll
     for (int i = 0; i < P::UPT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
+      for (int j = 0; j < 4; ++j) xreg[i][j] = PX::ld(rx, uvoff[i] + (unsigned)j * chb, 0u);
   };
   auto store_x = [&](int buf, int c) {
     const f32x4 (&xreg)[P::UPT] = xall[ALLX ? c : 0];
@@ -396,7 +402,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
     if constexpr (POST) {
       post_epilogue(pa, acc, b, t0, mrow0, wn, lane);
     } else {
-      conv_epilogue<TM, TN, H3>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
+      conv_epilogue<TM, TN, H3, YB>(a2, acc, b, t0 + wn * TN * 32, mrow0, lane, t0 + RP_BN, bsm + C);
     }
   }
 }
@@ -407,15 +413,27 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
   // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32; GEO 2 double-buffers
   // (the LDS of three workgroups per CU)
   constexpr bool AX = C == 64 && GEO != 2;
-  if (a.post_w) {
-    using P = PairCfg<S, K, C, 2, GEO, AX, true>;
-    static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
-    dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
-    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, true>), grid, dim3(256), 0, s, a);
+  auto go = [&](auto pl_tag) {
+    constexpr int PL = decltype(pl_tag)::value;
+    if (a.post_w) {
+      using P = PairCfg<S, K, C, 2, GEO, AX, true>;
+      static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
+      dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
+      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, true, PL>), grid, dim3(256), 0, s, a);
+      return;
+    }
+    dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
+    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, false, PL>), grid, dim3(256), 0, s, a);
+  };
+  if (a.c1.planes != 0) {
+    // bf16 activation planes: x, x' and z all bf16 (the bf16 scheme)
+    constexpr bool OK = std::is_same<S, SchemeB1>::value;
+    TTS_REQUIRE(OK && a.c1.planes == (kPlaneXB16 | kPlaneYB16) && a.c2.planes == a.c1.planes, 3,
+                "resblock pair: bf16 planes need the bf16 scheme");
+    if constexpr (OK) go(std::integral_constant<int, kPlaneXB16 | kPlaneYB16>{});
     return;
   }
-  dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX>), grid, dim3(256), 0, s, a);
+  go(std::integral_constant<int, 0>{});
 }
 
 int pair_geo64() {
@@ -479,7 +497,7 @@ template <class S, int C, int GEO, int K>
 void launch_res3_t(const ResBlock3Args& a, int B, hipStream_t s) {
   using P = Res3Cfg<S, C, GEO, K, 6, r3_xoff(K), r3_lead(K)>;
   dim3 grid(ceil_div(a.T, P::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, K, 6, r3_xoff(K), r3_lead(K)>), grid, dim3(P::NT), 0, s, a);
+  launch_block_pl<S, C, GEO, K, 6, r3_xoff(K), r3_lead(K)>(a, grid, P::NT, s);
 }
 template <class S>
 void launch_res3_s(const ResBlock3Args& a, int B, int C, int K, hipStream_t s) {

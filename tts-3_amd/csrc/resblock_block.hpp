@@ -16,6 +16,8 @@
 // launches (ResBlock1) or two conv launches (ResBlock2): x is read once and z written once.
 // ---------------------------------------------------------------------------------------
 #pragma once
+#include <type_traits>
+
 #include "split_device.hpp"
 
 #ifndef RES_STAGE_8R
@@ -64,10 +66,14 @@ struct Res3Cfg {
 #ifndef RB3_W64
 #define RB3_W64 2  // A/B build option: waves per SIMD requested for the 64-channel 128-column block
 #endif
-template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD>
+// PL: ResBlock3Args::planes (the bf16 scheme: 0, or bf16 x and z planes; x stays fp32 in registers)
+template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD, int PL = 0>
 __global__ __launch_bounds__((Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>::NT))
 __attribute__((amdgpu_waves_per_eu(C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO == 3 ? 2 : 1))))
 void resblock3_kernel(ResBlock3Args a) {
+  constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
+  using PX = PlaneT<XB>;
+  using PY = PlaneT<YB>;
   using P = Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>;
   static_assert(NCV == 6 || NCV == 2, "ResBlock1 (6 convs) or ResBlock2 (2 convs)");
   constexpr int NP = S::NP;
@@ -93,9 +99,12 @@ void resblock3_kernel(ResBlock3Args a) {
   const int tx0 = t0 - LEAD;  // time of column 0
   const int xcol0 = wn * TN * 32 + l32;
   const unsigned avoff = (unsigned)lane * 16u;
-  const unsigned chb = (unsigned)T * 4u;
-  const float* xb = a.x + (size_t)b * C * T;
-  const rsrc_t rx = make_rsrc(xb, (unsigned)C * chb);
+  const unsigned chb = (unsigned)T * PX::ES;
+  const rsrc_t rx = make_rsrc(plane_at<XB>(a.x, (size_t)b * C * T), (unsigned)C * chb);
+  auto ldx = [&](unsigned off, auto pol_tag) -> float {
+    if constexpr (XB) return PX::ld(rx, off, 0u);
+    else return bload_x<decltype(pol_tag)::value>(rx, off, 0u);
+  };
 
   // ---- prologue: lrelu(x0) pieces for columns [-XO, RP_W + XO) of every 16-channel group, and x0
   // itself in the acc layout.  Every load is issued before the first store (one HBM latency for
@@ -124,9 +133,10 @@ void resblock3_kernel(ResBlock3Args a) {
         const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
         const int ts = tx0 - XO + r;
         const bool ok = r < PR && ts >= 0 && ts < T;
-        const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * 4u;
+        const unsigned vo = (unsigned)(16 * g + 4 * q) * chb + (unsigned)ts * PX::ES;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[g][i][j] = bload_x(rx, ok ? vo + (unsigned)j * chb : OOB_OFF, 0u);
+        for (int j = 0; j < 4; ++j)
+          xv[g][i][j] = ldx(ok ? vo + (unsigned)j * chb : OOB_OFF, std::integral_constant<int, TTS_LDX_POL>{});
       }
     // x0 in the acc layout (the residual): the same bytes as the window, so read once the window
     // has landed (L2 hits; issued together, both missed L2: 2.4x the x plane in FETCH_SIZE).  It is
@@ -141,7 +151,8 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            xr[m][n][r] = bload_x<R3_XR_POL>(rx, tok ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF, 0u);
+            xr[m][n][r] = ldx(tok ? (unsigned)co * chb + (unsigned)t * PX::ES : OOB_OFF,
+                              std::integral_constant<int, R3_XR_POL>{});
           }
         }
     };
@@ -318,7 +329,8 @@ void resblock3_kernel(ResBlock3Args a) {
   auto final_to_z = [&](int ci) {
     const float sc = H3 ? ldexpf(1.f, ex + a.w_exp[ci]) : 1.f;
     const float* bs = bsm + ci * C;
-    const rsrc_t rz = make_rsrc(a.z + (size_t)b * C * T, (unsigned)C * chb);
+    const unsigned chbz = (unsigned)T * PY::ES;
+    const rsrc_t rz = make_rsrc(plane_at<YB>(a.z, (size_t)b * C * T), (unsigned)C * chbz);
     float vmax = 0.f;
 #pragma unroll
     for (int m = 0; m < TM; ++m) {
@@ -335,8 +347,8 @@ void resblock3_kernel(ResBlock3Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = mrow0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          vo[r] = keep ? (unsigned)co * chb + (unsigned)t * 4u : OOB_OFF;
-          zv[r] = a.zmode >= 2 ? bload(rz, vo[r], 0u) : 0.f;
+          vo[r] = keep ? (unsigned)co * chbz + (unsigned)t * PY::ES : OOB_OFF;
+          zv[r] = a.zmode >= 2 ? PY::ld(rz, vo[r], 0u) : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -344,7 +356,7 @@ void resblock3_kernel(ResBlock3Args a) {
           if (a.zmode == 2) v = zv[r] + v;
           else if (a.zmode == 3) v = (zv[r] + v) / a.zdiv;
           if (keep) vmax = fmaxf(vmax, fabsf(v));
-          bstore(rz, v, vo[r], 0u);
+          PY::st(rz, v, vo[r], 0u);
         }
       }
     }
@@ -415,12 +427,24 @@ namespace tts {
 // ResBlock2 launchers (one translation unit per split scheme: kernels_resblock2_{h3,b1,x6}.hip).
 // Geometry: C = 32 256 columns, C = 64 128 columns (geo64 = 1: 192), C = 128 128 columns as 8
 // waves (kernels 3 and 5 only: 7 and 11 take Winograd F(4,4) per conv at >= 128 channels).
+// the launch of one whole-block instance, with its bf16-plane form when ResBlock3Args::planes asks
+template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD>
+void launch_block_pl(const ResBlock3Args& a, dim3 grid, int nt, hipStream_t s) {
+  if (a.planes != 0) {
+    constexpr bool OK = std::is_same<S, SchemeB1>::value;
+    TTS_REQUIRE(OK && a.planes == (kPlaneXB16 | kPlaneYB16), 3, "resblock block: bf16 planes need the bf16 scheme");
+    if constexpr (OK)
+      hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, K, NCV, XO, LEAD, kPlaneXB16 | kPlaneYB16>), grid, dim3(nt), 0, s, a);
+    return;
+  }
+  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, K, NCV, XO, LEAD>), grid, dim3(nt), 0, s, a);
+}
 template <class S, int C, int GEO, int K>
 void launch_rb2_t(const ResBlock3Args& a, int B, hipStream_t s) {
   constexpr int H = rb2_halo(K);
   using P = Res3Cfg<S, C, GEO, K, 2, H, H>;
   dim3 grid(ceil_div(a.T, P::RP_BN), 1, B);
-  hipLaunchKernelGGL((resblock3_kernel<S, C, GEO, K, 2, H, H>), grid, dim3(P::NT), 0, s, a);
+  launch_block_pl<S, C, GEO, K, 2, H, H>(a, grid, P::NT, s);
 }
 template <class S, int C, int GEO>
 void launch_rb2_k(const ResBlock3Args& a, int B, int K, hipStream_t s) {

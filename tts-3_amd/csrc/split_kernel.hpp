@@ -3,6 +3,8 @@
 // See kernels_conv_split.hip for the algorithm, the tile table and the selection.
 #pragma once
 
+#include <type_traits>
+
 #include "split_device.hpp"
 
 namespace tts {
@@ -96,11 +98,16 @@ __device__ __forceinline__ void gate_epilogue(const Conv1dArgs& args, const f32x
   if (H3 && a.amax_out) publish_amax(a.amax_out, b, vm);
 }
 
-template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD, bool GATE = false>
+// PL: Conv1dArgs::planes as a template parameter (kPlaneXB16: bf16 input, kPlaneYB16: bf16
+// outputs / residual / MRF sum); only the MATH_BF16 scheme instantiates PL != 0
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD, bool GATE = false, int PL = 0>
 __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   using C = SplitCfg<S, K, BM, BN, TM, TN, G, HMAX, PD>;
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
+  constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
+  using PX = PlaneT<XB>;
+  static_assert(PL == 0 || (!GATE && !H3), "bf16 planes: plain epilogues of the bf16 scheme only");
   // the gate epilogue reuses the staging buffers for its sigmoid exchange (32 KiB)
   constexpr int XCHB = GATE ? 4 * C::WN * TM * TN * 16 * 64 : 0;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::XSZB > XCHB ? 2 * C::XSZB : XCHB];
@@ -134,8 +141,8 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
   // x of batch item b; one buffer descriptor per chunk (scalar ops), every range-checked
   // offset in the per-lane voffset: zero rows and channels >= Cin read 0 through the hardware
   // range check instead of per-element selects
-  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
-  const unsigned chb = (unsigned)Tin * 4u;  // bytes per channel row
+  const char* xb = static_cast<const char*>(plane_at<XB>(a.x, (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin)));
+  const unsigned chb = (unsigned)Tin * PX::ES;  // bytes per channel row
 
   // staging units (chunk invariant): unit u -> channel quad q, row r, group g.  SPLIT_STAGE_8R: a
   // 16-lane store group writes 8 consecutive rows x 2 quad positions; the row pitches (80 / 112 /
@@ -156,18 +163,18 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     const bool ok = (g < G) && ts >= 0 && ts < (a.rep_pad ? Tout : Tin);
     int src = ts - a.rep_pad;
     src = src < 0 ? 0 : (src >= Tin ? Tin - 1 : src);
-    uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * 4u : OOB_OFF;
+    uvoff[i] = ok ? (unsigned)(16 * g + 4 * q) * chb + (unsigned)src * PX::ES : OOB_OFF;
     ulds[i] = (g < G) ? (g * C::XROWS + r) * S::ROWB + 8 * quad_pos(q) : -1;
   }
 
   f32x4 xreg[C::UPT];
   auto load_x = [&](int c) {
     const int c0 = c * C::CK;
-    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * chb, (unsigned)(Cin - c0) * chb);
 #pragma unroll
     for (int i = 0; i < C::UPT; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xreg[i][j] = bload(rx, uvoff[i] + (unsigned)j * chb, 0u);
+      for (int j = 0; j < 4; ++j) xreg[i][j] = PX::ld(rx, uvoff[i] + (unsigned)j * chb, 0u);
     }
   };
   auto store_x = [&](int buf) {
@@ -308,21 +315,22 @@ __global__ __launch_bounds__(256) void conv1d_split_kernel(Conv1dArgs a) {
     static_assert(BM == 128 && C::WM == 2, "gate epilogue");
     gate_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt, wm, wn, lane, reinterpret_cast<float*>(smem));
   } else if constexpr (K == 2) {
-    convT_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr, SB ? scvec : nullptr, mt * BM);
+    convT_epilogue<TM, TN, H3, YB>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr, SB ? scvec : nullptr, mt * BM);
   } else {
     if constexpr (K == 1) {
-      if (a.wn_rows) {
+      if (!YB && a.wn_rows) {
         conv_epilogue_wn<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, SB ? sbias : nullptr,
                                      mt * BM);
         return;
       }
     }
-    conv_epilogue<TM, TN, H3>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, 0x7fffffff, SB ? sbias : nullptr, mt * BM);
+    conv_epilogue<TM, TN, H3, YB>(a, acc[0], b, t0 + wn * TN * 32, mt * BM + wm * TM * 32, lane, 0x7fffffff, SB ? sbias : nullptr, mt * BM);
   }
 }
 
 namespace split_detail {
-template <class S, int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE, bool GATE = false>
+// PLV: this tile has bf16-plane instances (the MATH_BF16 tile choices, conv1d_split_tile_for)
+template <class S, int K, int BM, int BN, int TM, int TN, int G, int PD, bool WIDE, bool GATE = false, bool PLV = false>
 void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
   dim3 grid(ceil_div(a.Tout, BN), ceil_div(a.Cout, BM), B);
   const int halo = (K - 1) * a.dil;
@@ -338,6 +346,30 @@ void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
   TTS_REQUIRE(a.wn_rows == 0 || (K == 1 && a.wn_rows % 32 == 0 && a.Cout == 2 * a.wn_rows && a.mask && a.z &&
                                  a.y && (a.zmode == 1 || a.zmode == 2) && a.ups == 0),
               1, "conv1d(split): bad WaveNet update-epilogue arguments");
+  if (a.planes != 0) {
+    // bf16 activation planes: the bf16 scheme's HiFiGAN tiles; x fp32 -> y bf16 only for conv_pre (K 7)
+    constexpr bool OK = std::is_same<S, SchemeB1>::value && PLV && K != 1;
+    TTS_REQUIRE(OK && a.wn_rows == 0 && !a.mask && (a.planes == (kPlaneXB16 | kPlaneYB16) || (a.planes == kPlaneYB16 && K == 7)),
+                3, "conv1d(split): bf16 planes are not built for this tile / kernel size");
+    if constexpr (OK) {
+      auto go = [&](auto pl_tag) {
+        constexpr int PLc = decltype(pl_tag)::value;
+        if (halo <= (K - 1) * 5) {
+          hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD, false, PLc>), grid, dim3(256), 0, s, a);
+        } else if (WIDE && halo <= 96) {
+          hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, WIDE ? 96 : 0, PD, false, PLc>), grid, dim3(256), 0, s, a);
+        } else {
+          throw Error(3, "conv1d(split): (kernel_size-1)*dilation = " + std::to_string(halo) + " too large for this tile");
+        }
+      };
+      if (a.planes == kPlaneYB16) {
+        if constexpr (K == 7) go(std::integral_constant<int, kPlaneYB16>{});
+      } else {
+        go(std::integral_constant<int, kPlaneXB16 | kPlaneYB16>{});
+      }
+    }
+    return;
+  }
   if (halo <= (K - 1) * 5) {
     hipLaunchKernelGGL((conv1d_split_kernel<S, K, BM, BN, TM, TN, G, (K - 1) * 5, PD>), grid, dim3(256), 0, s, a);
   } else if (WIDE && halo <= 96) {
@@ -350,21 +382,21 @@ void launch_split_t(const Conv1dArgs& a, int B, hipStream_t s) {
 template <class S, int K>
 void launch_split_k(const Conv1dArgs& a, int B, int tile, hipStream_t s) {
   switch (tile) {
-    case 0: launch_split_t<S, K, 128, 128, 2, 2, 1, 1, true>(a, B, s); break;
-    case 1: launch_split_t<S, K, 64, 256, 2, 2, 1, 1, true>(a, B, s); break;
-    case 2: launch_split_t<S, K, 32, 512, 1, 4, 1, 1, true>(a, B, s); break;
-    case 3: launch_split_t<S, K, 128, 128, 2, 2, 2, 1, false>(a, B, s); break;
+    case 0: launch_split_t<S, K, 128, 128, 2, 2, 1, 1, true, false, true>(a, B, s); break;
+    case 1: launch_split_t<S, K, 64, 256, 2, 2, 1, 1, true, false, true>(a, B, s); break;
+    case 2: launch_split_t<S, K, 32, 512, 1, 4, 1, 1, true, false, true>(a, B, s); break;
+    case 3: launch_split_t<S, K, 128, 128, 2, 2, 2, 1, false, false, true>(a, B, s); break;
     case 4: launch_split_t<S, K, 64, 128, 2, 1, 2, 1, false>(a, B, s); break;
     case 5: launch_split_t<S, K, 32, 256, 1, 2, 2, 1, false>(a, B, s); break;
     case 6: launch_split_t<S, K, 64, 256, 2, 2, 2, 1, false>(a, B, s); break;
-    case 7: launch_split_t<S, K, 128, 128, 2, 2, 1, 2, false>(a, B, s); break;
+    case 7: launch_split_t<S, K, 128, 128, 2, 2, 1, 2, false, false, true>(a, B, s); break;
     case 8: launch_split_t<S, K, 64, 128, 2, 1, 2, 2, false>(a, B, s); break;
     case 9: launch_split_t<S, K, 64, 256, 2, 2, 2, 2, false>(a, B, s); break;
-    case 10: launch_split_t<S, K, 64, 256, 2, 2, 1, 2, false>(a, B, s); break;
+    case 10: launch_split_t<S, K, 64, 256, 2, 2, 1, 2, false, false, true>(a, B, s); break;
     case 11: launch_split_t<S, K, 32, 256, 1, 2, 2, 2, false>(a, B, s); break;
     case 12: launch_split_t<S, K, 64, 128, 2, 1, 2, 3, false>(a, B, s); break;
-    case 13: launch_split_t<S, K, 128, 128, 2, 2, 2, 2, false>(a, B, s); break;
-    case 14: launch_split_t<S, K, 32, 256, 1, 2, 1, 1, false>(a, B, s); break;
+    case 13: launch_split_t<S, K, 128, 128, 2, 2, 2, 2, false, false, true>(a, B, s); break;
+    case 14: launch_split_t<S, K, 32, 256, 1, 2, 1, 1, false, false, true>(a, B, s); break;
     case 15: launch_split_t<S, K, 32, 256, 1, 2, 1, 2, false>(a, B, s); break;
     case 16: launch_split_t<S, K, 32, 128, 1, 1, 1, 2, false>(a, B, s); break;
     case 17: launch_split_t<S, K, 64, 128, 2, 1, 1, 1, false>(a, B, s); break;

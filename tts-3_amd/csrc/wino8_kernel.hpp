@@ -40,8 +40,12 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
     }                                                                                                        \
   } while (0)
 
-template <class S, int K, int D>
+// XB: the input plane is bf16 (Conv1dArgs::planes, MATH_BF16): the raw window in LDS holds 2-byte
+// elements, AL = 8 per 16-byte DMA unit instead of 4
+template <class S, int K, int D, bool XB = false>
 struct Wino8Cfg {
+  static constexpr int ES = XB ? 2 : 4;              // bytes per raw element
+  static constexpr int AL = 16 / ES;                 // raw elements per 16-byte DMA unit
   static constexpr int NCH = wino_chunks(K);
   static constexpr int NS = kWinoPoints * NCH;       // packed steps per 16-channel chunk (c*7 + p)
   static constexpr int PAD = D * (K - 1) / 2;
@@ -51,12 +55,15 @@ struct Wino8Cfg {
   static constexpr int XROWS = BNT + (NCH - 1) * D;  // transformed columns (halo of the chunk shifts)
   static constexpr int PLANE = XROWS * S::ROWB;
   static constexpr int TSZ = kWinoPoints * PLANE;    // bytes of one transformed buffer
-  // raw window: times t0 - PAD - ROFF ... (16-byte aligned start; t0 is a multiple of 4)
-  static constexpr int ROFF = (4 - PAD % 4) % 4;
+  // raw window: times t0 - PAD - ROFF ... (16-byte aligned start; t0 is a multiple of 4, of 8 but at
+  // D = 3 (TW = 252), where the bf16 form takes its offset per workgroup: roff <= 7, span for 7)
+  static constexpr bool RT_ROFF = XB && TW % 8 != 0;
+  static constexpr int ROFF = RT_ROFF ? 7 : (AL - PAD % AL) % AL;
   static constexpr int RSPAN = (XROWS - 1) % D + 4 * D * ((XROWS - 1) / D) + 6 * D + ROFF + 1;
-  static constexpr int RSPAN4 = (RSPAN + 3) / 4 * 4;
-  static constexpr int RPITCH = RSPAN4 % 8 == 4 ? RSPAN4 : RSPAN4 + 4;  // RPITCH / 4 odd
-  static constexpr int RF4 = (16 * RPITCH / 4 + 63) / 64 * 64;          // float4s per raw buffer (DMA rows of 64)
+  static constexpr int RSPAN4 = (RSPAN + AL - 1) / AL * AL;
+  // RPITCH / AL odd: the 16-byte units of consecutive channel rows cycle through the bank row
+  static constexpr int RPITCH = RSPAN4 % (2 * AL) == AL ? RSPAN4 : RSPAN4 + AL;
+  static constexpr int RF4 = (16 * RPITCH / AL + 63) / 64 * 64;         // 16-byte units per raw buffer (DMA rows of 64)
   static constexpr int RSZ = RF4 * 16;
   static constexpr int NDMA = RF4 / 64;              // DMA instructions per chunk (waves 4-7)
   static constexpr int UNITS = XROWS * 4;            // (column, channel quad)
@@ -71,12 +78,15 @@ struct Wino8Cfg {
   static constexpr int TSM = 2 * TSZ > EPI ? 2 * TSZ : EPI;
 };
 
-template <class S, int K, int D, bool LRELU>
+// PL: Conv1dArgs::planes (MATH_BF16 only: 0, or bf16 input and bf16 res / z / y)
+template <class S, int K, int D, bool LRELU, int PL = 0>
 __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
-  using C = Wino8Cfg<S, K, D>;
+  constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
+  using C = Wino8Cfg<S, K, D, XB>;
   constexpr int NP = S::NP;
   constexpr int NCH = C::NCH;
   constexpr bool H3 = S::SCALED;
+  static_assert(PL == 0 || !H3, "bf16 planes: the bf16 scheme only");
 // weight prefetch depths (steps) of the two point groups and the transform-piece read->math gap
 // (steps) per kernel size; round-4 re-tune after the conflict-free job reads (3 rounds x 3 builds,
 // one box session): PD 3 / PD1 4 / GAP11 1 gave 53.5 ms per batch against 53.9 for the round-3
@@ -119,24 +129,26 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const int ex = H3 ? amax_exp(a.amax_in, b) + kWinoBtShift : 0;
   const float xscale = H3 ? ldexpf(1.f, -ex) : 1.f;
   const float slope = a.in_slope;
-  const float* xb = a.x + (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin);
-  const unsigned chb = (unsigned)Tin * 4u;
+  const char* xb = static_cast<const char*>(plane_at<XB>(a.x, (size_t)b * (a.x_bstride ? a.x_bstride : (int64_t)Cin * Tin)));
+  const unsigned chb = (unsigned)Tin * (unsigned)C::ES;
 
-  // ---- input DMA (waves 4-7): raw[ch][RPITCH] fp32, window start ta = t0 - PAD - ROFF ----
-  const int ta = t0 - C::PAD - C::ROFF;
+  // ---- input DMA (waves 4-7): raw[ch][RPITCH] elements, window start ta = t0 - PAD - roff ----
+  const int roff = C::RT_ROFF ? (((t0 - C::PAD) % 8) + 8) % 8 : C::ROFF;  // ta = 0 mod AL
+  const int ta = t0 - C::PAD - roff;
   // DMA instructions i = wm + 4k of raw(c) -> R[rb], for k in [k0, k1) (wave-uniform)
 #ifndef WINO8_ASM_DMA
 #define WINO8_ASM_DMA 1  // 0: the LDS-DMA builtin (the compiler then waits for each DMA at the next LDS access)
 #endif
   auto dma = [&](int c, int rb, int k0 = 0, int k1 = 64) {
     const int c0 = c * 16;
-    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb);
+    const rsrc_t rx = make_rsrc(xb + (size_t)c0 * chb, (unsigned)(Cin - c0) * chb);
     for (int i = wm + 4 * k0; i < C::NDMA && i < wm + 4 * k1; i += 4) {
       const int f = i * 64 + lane;
-      const int ch = f / (C::RPITCH / 4), t = ta + 4 * (f - ch * (C::RPITCH / 4));
-      const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * 4u : OOB_OFF;
+      constexpr int UPR = C::RPITCH / C::AL;  // 16-byte units per channel row
+      const int ch = f / UPR, t = ta + C::AL * (f - ch * UPR);
+      const unsigned vo = (ch < 16 && t >= 0 && t < Tin) ? (unsigned)ch * chb + (unsigned)t * (unsigned)C::ES : OOB_OFF;
       if (WINO8_ASM_DMA) {
-        lds_dma_b128(xb + (size_t)c0 * Tin, (unsigned)(Cin - c0) * chb, vo, rsm + rb * C::RSZ + i * 1024);
+        lds_dma_b128(xb + (size_t)c0 * chb, (unsigned)(Cin - c0) * chb, vo, rsm + rb * C::RSZ + i * 1024);
       } else {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rx, (__attribute__((address_space(3))) void*)(rsm + rb * C::RSZ + i * 1024), 16, (int)vo, 0, 0, 0);
@@ -175,9 +187,11 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // D = 1: a column's 7 inputs are raw floats 4 urow + ROFF ... + 6 of its channel row, read as NU
   // aligned float4s (ds_read_b128).  The lanes of a 16-lane group hold 4 columns x 4 channel quads:
   // float4 slots c * RPITCH / 4 + urow, RPITCH / 4 odd, cover all 16 slots of the bank row (no
-  // conflict), where 7 ds_read_b32 at one sub-offset put 32 lanes on 8 banks (4-way)
+  // conflict), where 7 ds_read_b32 at one sub-offset put 32 lanes on 8 banks (4-way).  bf16 input:
+  // NU 8-byte groups of 4 elements (ds_read_b64), widened in job_finish
   constexpr int NU = (C::ROFF + 6) / 4 + 1;
-  f32x4 jraw4[NU];
+  f32x4 jraw4[XB ? 1 : NU];
+  u32x2_t jraw8[XB ? NU : 1];
   // piece j: channel 4q + j; pairs are written after channels 1 and 3.  A piece runs in two parts
   // one MFMA step apart: job_load issues its 7 LDS reads, job_finish transforms (and splits and
   // stores every second piece), so the reads' latency hides behind the step's MFMAs
@@ -213,11 +227,22 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     if (!uok) return;
     int jrow, jq;
     job_unit(jrow, jq);
-    if constexpr (D == 1) {
+    if constexpr (D == 1 && XB) {
+      const u32x2_t* raw8 =
+          reinterpret_cast<const u32x2_t*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * (C::RPITCH / 4) + jrow;
+#pragma unroll
+      for (int u4 = 0; u4 < NU; ++u4) jraw8[u4] = raw8[u4];
+    } else if constexpr (D == 1) {
       const f32x4* raw4 =
           reinterpret_cast<const f32x4*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * (C::RPITCH / 4) + jrow;
 #pragma unroll
       for (int u4 = 0; u4 < NU; ++u4) jraw4[u4] = raw4[u4];
+    } else if constexpr (XB) {
+      const int jjj = jrow / D, jrho = jrow - jjj * D;
+      const unsigned short* raw = reinterpret_cast<const unsigned short*>(rsm + rb * C::RSZ) +
+                                  (4 * jq + piece(j)) * C::RPITCH + jrho + 4 * D * jjj + roff;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) jraw[k] = bf16_bits_to_f32(raw[D * k]);
     } else {
       const int jjj = jrow / D, jrho = jrow - jjj * D;
       const float* raw = reinterpret_cast<const float*>(rsm + rb * C::RSZ) + (4 * jq + piece(j)) * C::RPITCH +
@@ -234,7 +259,13 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     float v[7], t[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      float x = D == 1 ? jraw4[(C::ROFF + k) / 4][(C::ROFF + k) % 4] : jraw[k];
+      float x;
+      if constexpr (D == 1 && XB) {
+        const unsigned w = jraw8[(C::ROFF + k) / 4][((C::ROFF + k) % 4) / 2];
+        x = bf16_bits_to_f32((C::ROFF + k) % 2 ? w >> 16 : w & 0xffffu);
+      } else {
+        x = D == 1 ? jraw4[(C::ROFF + k) / 4][(C::ROFF + k) % 4] : jraw[k];
+      }
       if (LRELU) x = lrelu2(x, slope);
       v[k] = H3 ? x * xscale : x;
     }
@@ -473,11 +504,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     constexpr int ZM = decltype(zm_tag)::value;
     const int Cout = a.Cout;
     const int Tout = a.Tout;
-    const unsigned plane = (unsigned)Cout * (unsigned)Tout * 4u;
+    constexpr unsigned YES = PlaneT<YB>::ES;
+    const unsigned plane = (unsigned)Cout * (unsigned)Tout * YES;
     const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)Cout * Tout);
-    const rsrc_t rres = make_rsrc(RES ? a.res + item : a.bias, RES ? plane : 0u);
-    const rsrc_t rz = make_rsrc(ZM >= 2 ? a.z + item : a.bias, ZM >= 2 ? plane : 0u);
-    const rsrc_t rout = make_rsrc((a.zmode == 0 ? a.y : a.z) + item, plane);
+    const rsrc_t rres = make_rsrc(RES ? plane_at<YB>(a.res, item) : a.bias, RES ? plane : 0u);
+    const rsrc_t rz = make_rsrc(ZM >= 2 ? plane_at<YB>(a.z, item) : a.bias, ZM >= 2 ? plane : 0u);
+    const rsrc_t rout = make_rsrc(plane_at<YB>(a.zmode == 0 ? a.y : a.z, item), plane);
     const float oslope = a.out_slope;
     const float zdiv = a.zdiv;
     float vmax = 0.f;
@@ -499,15 +531,15 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
           const int r = r0 + k;
           const unsigned co = (unsigned)(cobase + (r & 3) + 8 * (r >> 2) + 4 * half);
           bias[k] = wbias[co - (unsigned)(mt * 128)];
-          voff[k] = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-          gin[k] = wino_gather<RES, ZM>(rres, rz, voff[k], full, nvalid);
+          voff[k] = nvalid > 0 ? (co * (unsigned)Tout + (unsigned)t) * YES : OOB_OFF;
+          gin[k] = wino_gather<RES, ZM, YB>(rres, rz, voff[k], full, nvalid);
         }
 #pragma unroll
         for (int k = 0; k < GR; ++k) {
           const int r = r0 + k;
           const f32x4 yv = {y[0][r], y[1][r], y[2][r], y[3][r]};
           const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[k], oslope, zdiv, gin[k], nvalid, vmax, sc);
-          wino_store(rout, v, voff[k], full, nvalid);
+          wino_store<YB>(rout, v, voff[k], full, nvalid);
         }
       }
     } else {
@@ -538,14 +570,14 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
         for (int rr = 0; rr < 8; ++rr) {
           const int co = cobase + 16 * ps + grp * 8 + rr;
           bias[rr] = wbias[co - mt * 128];
-          voff[rr] = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * 4u : OOB_OFF;
-          gin[rr] = wino_gather<RES, ZM>(rres, rz, voff[rr], full, nvalid);
+          voff[rr] = nvalid > 0 ? ((unsigned)co * (unsigned)Tout + (unsigned)t) * YES : OOB_OFF;
+          gin[rr] = wino_gather<RES, ZM, YB>(rres, rz, voff[rr], full, nvalid);
         }
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
           const f32x4 yv = *reinterpret_cast<const f32x4*>(tile + (grp * 8 + rr) * C::PITCH + tl);
           const f32x4 v = wino_apply<RES, ZM, H3>(yv, bias[rr], oslope, zdiv, gin[rr], nvalid, vmax, sc);
-          wino_store(rout, v, voff[rr], full, nvalid);
+          wino_store<YB>(rout, v, voff[rr], full, nvalid);
         }
         lds_sync();
       }
@@ -574,6 +606,23 @@ template <class S, int K, int D>
 void launch_d(const Conv1dArgs& a, int B, hipStream_t s) {
   using C = Wino8Cfg<S, K, D>;
   const dim3 grid(ceil_div(a.Tout, C::TW), ceil_div(a.Cout, 128), B);
+  if (a.planes != 0) {
+    // bf16 activation planes (MATH_BF16): 16-byte aligned bf16 rows
+    constexpr bool OK = std::is_same<S, SchemeB1>::value;
+    TTS_REQUIRE(OK && a.planes == (kPlaneXB16 | kPlaneYB16) && a.Tin % 8 == 0, 3,
+                "conv1d(winograd8): bf16 planes need the bf16 scheme and T % 8 == 0");
+    if constexpr (OK) {
+      constexpr int PL = kPlaneXB16 | kPlaneYB16;
+      if constexpr (D == 1) {
+        if (a.in_slope == 1.f) {
+          hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, false, PL>), grid, dim3(512), 0, s, a);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, true, PL>), grid, dim3(512), 0, s, a);
+    }
+    return;
+  }
   if constexpr (D == 1) {
     if (a.in_slope == 1.f) {
       hipLaunchKernelGGL((conv1d_wino8_kernel<S, K, D, false>), grid, dim3(512), 0, s, a);

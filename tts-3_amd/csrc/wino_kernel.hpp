@@ -109,20 +109,21 @@ struct WinoCfg {
 struct WinoIn {
   f32x4 rv, zv;
 };
-template <bool RES, int ZM>
+template <bool RES, int ZM, bool YB = false>
 __device__ __forceinline__ WinoIn wino_gather(const rsrc_t& rres, const rsrc_t& rz, unsigned voff, bool full, int nvalid) {
+  using PY = PlaneT<YB>;
   WinoIn g;
   g.rv = f32x4{};
   g.zv = f32x4{};
   if (full) {
-    if (RES) g.rv = bload4(rres, voff, 0u);
-    if (ZM >= 2) g.zv = bload4(rz, voff, 0u);
+    if (RES) g.rv = pload4<YB>(rres, voff, 0u);
+    if (ZM >= 2) g.zv = pload4<YB>(rz, voff, 0u);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const unsigned o = j < nvalid ? voff + 4u * j : OOB_OFF;
-      if (RES) g.rv[j] = bload(rres, o, 0u);
-      if (ZM >= 2) g.zv[j] = bload(rz, o, 0u);
+      const unsigned o = j < nvalid ? voff + PY::ES * j : OOB_OFF;
+      if (RES) g.rv[j] = PY::ld(rres, o, 0u);
+      if (ZM >= 2) g.zv[j] = PY::ld(rz, o, 0u);
     }
   }
   return g;
@@ -145,12 +146,14 @@ __device__ __forceinline__ f32x4 wino_apply(f32x4 y, float bias, float oslope, f
   return v;
 }
 
+template <bool YB = false>
 __device__ __forceinline__ void wino_store(const rsrc_t& rout, f32x4 v, unsigned voff, bool full, int nvalid) {
+  using PY = PlaneT<YB>;
   if (full) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rout, (int)voff, 0, TTS_ST_POL);
+    pstore4<YB>(rout, v, voff, 0u);
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bstore(rout, v[j], j < nvalid ? voff + 4u * j : OOB_OFF, 0u);
+    for (int j = 0; j < 4; ++j) PY::st(rout, v[j], j < nvalid ? voff + PY::ES * j : OOB_OFF, 0u);
   }
 }
 
