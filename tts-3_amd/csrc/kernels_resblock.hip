@@ -413,17 +413,18 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
   // all-at-once staging measured faster at 64 channels (-7% on k3), not at 32; GEO 2 double-buffers
   // (the LDS of three workgroups per CU)
   constexpr bool AX = C == 64 && GEO != 2;
+  constexpr int PD = S::NP == 1 ? RES_PD_B1 : 2;
   auto go = [&](auto pl_tag) {
     constexpr int PL = decltype(pl_tag)::value;
     if (a.post_w) {
-      using P = PairCfg<S, K, C, 2, GEO, AX, true>;
+      using P = PairCfg<S, K, C, PD, GEO, AX, true>;
       static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
       dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
-      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, true, PL>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, true, PL>), grid, dim3(256), 0, s, a);
       return;
     }
-    dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, 2, GEO>::RP_BN), 1, B);
-    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, 2, GEO, AX, false, PL>), grid, dim3(256), 0, s, a);
+    dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, PD, GEO>::RP_BN), 1, B);
+    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, false, PL>), grid, dim3(256), 0, s, a);
   };
   if (a.c1.planes != 0) {
     // bf16 activation planes: x, x' and z all bf16 (the bf16 scheme)

@@ -20,6 +20,9 @@
 
 #include "split_device.hpp"
 
+#ifndef RES_PD_B1
+#define RES_PD_B1 2  // weight prefetch depth of the whole-block and pair kernels in the bf16 scheme
+#endif
 #ifndef RES_STAGE_8R
 #define RES_STAGE_8R 1  // x staging lane map of the pair / whole-block kernels (0: 4 rows x 4 quads)
 #endif
@@ -79,7 +82,7 @@ void resblock3_kernel(ResBlock3Args a) {
   constexpr int NP = S::NP;
   constexpr bool H3 = S::SCALED;
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC, PR = P::PR, RP_W = P::RP_W;
-  constexpr int PD = 2;
+  constexpr int PD = S::NP == 1 ? RES_PD_B1 : 2;  // weight prefetch steps (bf16: its own, A/B)
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
   constexpr int NT = P::NT;
   __shared__ float red[2][P::NW];  // double-buffered: consecutive tile_exp calls use different halves

@@ -103,6 +103,12 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #ifndef WINO8_PD11
 #define WINO8_PD11 WINO8_PD  // kernel 11, points 0-3 (A/B: 2 keeps the kernel below 256 VGPRs)
 #endif
+#ifndef WINO8_PD_B1
+#define WINO8_PD_B1 3
+#endif
+#ifndef WINO8_PD1_B1
+#define WINO8_PD1_B1 4
+#endif
 #ifndef WINO8_GAP7
 #define WINO8_GAP7 1
 #endif
@@ -344,7 +350,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
     // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
     // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
-    constexpr int PD = P0 > 0 ? WINO8_PD1 : (K == 11 ? WINO8_PD11 : WINO8_PD);
+    // the bf16 scheme's steps are a third as long (one product per MAC): its own depths (A/B)
+    constexpr int PD = NP == 1 ? (P0 > 0 ? WINO8_PD1_B1 : WINO8_PD_B1)
+                               : (P0 > 0 ? WINO8_PD1 : (K == 11 ? WINO8_PD11 : WINO8_PD));
     // steps between a transform piece's LDS reads and its math (no later than the next piece's
     // reads); measured per kernel size
     constexpr int GAP0 = K == 11 ? WINO8_GAP11 : WINO8_GAP7;
