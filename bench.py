@@ -158,6 +158,12 @@ def algorithm_ratio(fam_name: str):
     return "winograd F(4,4)", 7 * ((K + 3) // 4) / 4 / K
 
 
+def activation_planes(mode: str) -> str:
+    """Element type of the HiFiGAN executor's activation planes in HBM (bf16 in the bf16 scheme unless
+    TTS_MI355X_BF16_PLANES=0, hifigan.hpp planes16_)."""
+    return "bf16" if mode == "bf16" and os.environ.get("TTS_MI355X_BF16_PLANES", "1") != "0" else "fp32"
+
+
 def family_roofline(rows, mode: str):
     """The dominant kernel family of one profiled forward against the dense peak of the matrix pipe
     its arithmetic issues on (the headline's roofline definition, for the side lines)."""
@@ -427,13 +433,17 @@ def glow_tts_e2e_bench(dev, modes, steps=10, warmup=3, B=16, T_x=128):
         torch.cuda.synchronize(dev)
         ms_glow = (time.perf_counter() - e0) / steps * 1e3
         _, erows = m.encoder.profile(tok, lens)
+        # the vocoder's kernels on a mel of the same shape (one profiled forward, serial schedule)
+        _, vrows = voc.profile(mel)
         out["mel_frames"] = int(mel.shape[2])
         out["variants"][label] = {
             "glow_decoder_math_mode": dmode, "vocoder_math_mode": vmode,
+            "vocoder_activation_planes": activation_planes(vmode),
             "ms_per_step": ms, "samples_per_s": samples / (ms / 1e3),
             "rtf": (ms / 1e3) / (samples / SAMPLE_RATE),
             "glow_tts_inference_ms": ms_glow,
             "encoder_kernel_ms": sum(r["ms"] for r in erows), "encoder_launches": len(erows),
+            "vocoder_roofline": family_roofline(vrows, vmode),
         }
         del m, voc, syn
     return out
@@ -515,7 +525,8 @@ def vits_bench(dev, steps=10, warmup=3, B=8, T=1024, cond=256):
         ms = (time.perf_counter() - t0) / steps * 1e3
         z = flow(zp, mask, g=g, reverse=True) * mask
         _, rows = dec.profile(z, g=g)
-        out["variants"][label] = {"flow_math_mode": fmode, "decoder_math_mode": dmode, "ms_per_step": ms,
+        out["variants"][label] = {"flow_math_mode": fmode, "decoder_math_mode": dmode,
+                                  "decoder_activation_planes": activation_planes(dmode), "ms_per_step": ms,
                                   "samples_per_s": wav.numel() / (ms / 1e3),
                                   "rtf": (ms / 1e3) / (wav.numel() / SAMPLE_RATE),
                                   "decoder_roofline": family_roofline(rows, dmode)}

@@ -68,8 +68,12 @@ struct PairCfg {
 // C = 32 (16-bit-pair schemes): ask for 3 waves per SIMD (<= 168 VGPRs + AGPRs): the LDS already
 // allows three workgroups per CU, the unconstrained allocation (173) allowed two
 // PL: the planes of x, x' / z (bf16 in the bf16 scheme's activation-plane form, Conv1dArgs::planes)
+#ifndef PAIR_W_B1
+#define PAIR_W_B1 3  // waves per SIMD asked of the bf16 scheme's pair kernels (0: as the others; 3 measured -1% per bf16 step, profiles/ab_r06_bf16_occupancy.txt)
+#endif
 template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false, int PL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    S::NP == 1 && PAIR_W_B1 > 0 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1))))
 void resblock_pair_kernel(ResPairArgs pa) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;

@@ -66,13 +66,17 @@ struct Res3Cfg {
   static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
+#ifndef RB3_W_B1
+#define RB3_W_B1 0  // A/B: waves per SIMD asked of the bf16 scheme's whole-block kernels (0: as the others)
+#endif
 #ifndef RB3_W64
 #define RB3_W64 2  // A/B build option: waves per SIMD requested for the 64-channel 128-column block
 #endif
 // PL: ResBlock3Args::planes (the bf16 scheme: 0, or bf16 x and z planes; x stays fp32 in registers)
 template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD, int PL = 0>
 __global__ __launch_bounds__((Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>::NT))
-__attribute__((amdgpu_waves_per_eu(C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO == 3 ? 2 : 1))))
+__attribute__((amdgpu_waves_per_eu(S::NP == 1 && RB3_W_B1 > 0 ? RB3_W_B1
+                                                                : (C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO == 3 ? 2 : 1)))))
 void resblock3_kernel(ResBlock3Args a) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;
