@@ -132,3 +132,26 @@ def test_bf16_planes_batch_invariant_and_deterministic(cuda_device, monkeypatch)
     for i in (0, 3):
         assert torch.equal(g.inference(mel[i:i + 1])[0], y[i])
     assert torch.isfinite(y).all() and y.abs().max() <= 1.0
+
+
+@pytest.mark.parametrize("planes", ["1", "0"])
+def test_bf16_pair128_matches_winograd(cuda_device, monkeypatch, planes):
+    """bf16: the 128-channel kernel-7 / 11 ResBlock1 iterations as fused pairs (resblock_pair128:
+    direct convs, xt in LDS; one launch per iteration) against the two Winograd launches per
+    iteration (TTS_MI355X_PAIR128=0), both within the bf16 gates of the fp64 oracle and of each
+    other, on either plane type; the profiled launch names show which form ran."""
+    monkeypatch.setenv("TTS_MI355X_BF16_PLANES", planes)
+    sd = synthetic.hifigan_state_dict(seed=66, weight_norm=False)
+    mel = synthetic.mel(2, 41, seed=10)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    outs = {}
+    for p128 in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_PAIR128", p128)
+        g = _gen(V1, sd, cuda_device)
+        outs[p128] = g.inference(mel.to(cuda_device)).cpu()
+        names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+        pairs = [n for n in names if n.startswith("mrf_pair_k") and n.endswith("_c128")]
+        winos = [n for n in names if n.startswith("mrf_wino_k") and n.endswith("_c128")]
+        assert (len(pairs), len(winos)) == ((6, 0) if p128 == "1" else (0, 12)), names
+        assert_close_fp32(outs[p128], ref, f"pair128={p128} planes={planes}", **tol("bf16"))
+    assert max_abs(outs["1"].numpy(), outs["0"].numpy()) <= 2 * tol("bf16")["max_abs_tol"]

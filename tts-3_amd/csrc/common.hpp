@@ -117,6 +117,7 @@ struct ResPairArgs {
 };
 bool resblock_pair_supported(int mode, int C, int K, int dil);
 bool resblock_pair_preferred(int mode, int C, int K, int dil);  // supported and measured faster
+bool resblock_pair128(int mode, int C, int K);  // bf16: 128-channel k7 / k11 iterations as pairs
 void launch_resblock_pair(int mode, const ResPairArgs& a, int B, int K, int C, hipStream_t s);
 
 // A whole kernel-3 ResBlock1 (three iterations, six convs) in one kernel (kernels_resblock.hip):

@@ -119,11 +119,22 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
               cfg_.upsample_factors[0] % 8 == 0;
   size_t wi = 0;
   std::vector<std::pair<const float*, const float*>> src;  // (w, b) per packed layer
-  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode) {
+  auto add_conv = [&](int Cin, int Cout, int K, int dil, const char* fam, bool res, int lmode, bool pair128 = false) {
     ConvLayer L;
     L.Cin = Cin; L.Cout = Cout; L.K = K; L.dil = dil; L.pad = dil * (K - 1) / 2;
     L.mode = lmode;
     L.tile = conv_tile_for(lmode, Cout, K, Cin, dil, res);
+    if (pair128) {
+      // a bf16 128-channel pair (resblock_pair128): the direct packing with 16-channel chunks
+      // (tile 7: 128 x 128, one 16-channel group per chunk) instead of the Winograd packing
+      L.tile = 7;
+      const ConvTile t = conv_tile(lmode, L.tile);
+      L.n_chunks = ceil_div(Cin, t.CK);
+      L.w_numel = packed_conv_numel(lmode, Cout, Cin, K, t);
+      L.b_numel = (int64_t)ceil_div(Cout, t.BM) * t.BM;
+      L.name = std::string(fam) + "_k" + std::to_string(K) + "_c" + std::to_string(Cout);
+      return L;
+    }
     // the MRF convs at >= 128 channels, kernels 7 and 11: Winograd F(4,4) (wino8_kernel.hpp;
     // MI355X, B=32: k11 c128 2.20 -> 1.73 ms, k7 c128 1.56 -> 1.43, k11 c256 1.16 -> 0.80, k7 c256
     // 0.82 -> 0.60 per launch; TTS_MI355X_WINO=0 keeps the direct kernel).  Kernel 3 is supported
@@ -187,13 +198,14 @@ Hifigan::Hifigan(const TtsHifiganCfg& cfg, const float* const* hw, int device)
         // fused convs1 -> convs2 iterations (kernels_resblock.hip) where supported; they reuse the
         // conv packing, which needs 32-row blocks covering the channels and 16-channel groups
         rb.fused = pair_fusion;
+        const bool p128 = pair_fusion && resblock_pair128(mode, ch, k);
         // the whole-block kernel reads the packing as [32-row block][16-channel group][tap]: the
         // conv tile must cover the channels without padding
         bool tiles_ok = true;
         for (int m = 0; m < 3; ++m) {
-          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false, mode));
+          rb.convs.push_back(add_conv(ch, ch, k, cfg_.resblock_dilation_sizes[j][m], "mrf_conv", false, mode, p128));
           src.push_back({w1[m], b1[m]});
-          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true, mode));
+          rb.convs.push_back(add_conv(ch, ch, k, 1, "mrf_conv", true, mode, p128));
           src.push_back({w2[m], b2[m]});
           for (int c = 0; c < 2; ++c) {
             const ConvTile t = conv_tile(mode, rb.convs[2 * m + c].tile);

@@ -73,7 +73,7 @@ struct PairCfg {
 #endif
 template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false, int PL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    S::NP == 1 && PAIR_W_B1 > 0 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1))))
+    S::NP == 1 && PAIR_W_B1 > 0 && C <= 64 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1))))
 void resblock_pair_kernel(ResPairArgs pa) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;
@@ -451,6 +451,15 @@ int pair_geo64() {
 
 template <class S, int K>
 void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
+  if constexpr (S::NP == 1) {
+    // bf16 only: 128 channels on 256 columns, one wave per SIMD (4 x 32 rows x 64 columns of
+    // accumulators per wave), the xt buffer 8 groups x 288 rows x 48 B = 111 KB (the 16-bit-pair
+    // schemes' 80-byte rows would need 184 KB)
+    if (C == 128) {
+      launch_pair_t<S, K, 128, 0>(a, B, s);
+      return;
+    }
+  }
   if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
   else if (C == 64 && pair_geo64() == 2 && S::ROWB <= 80) launch_pair_t<S, K, 64, 2>(a, B, s);
   else if (C == 64) launch_pair_t<S, K, 64, 1>(a, B, s);
@@ -469,7 +478,15 @@ void launch_pair_s(const ResPairArgs& a, int B, int K, int C, hipStream_t s) {
 }  // namespace
 
 bool resblock_pair_supported(int mode, int C, int K, int dil) {
-  return is_split_mode(mode) && (C == 32 || C == 64) && (K == 3 || K == 7 || K == 11) && dil >= 1 && dil <= 5;
+  return is_split_mode(mode) && (C == 32 || C == 64 || (C == 128 && mode == MATH_BF16)) &&
+         (K == 3 || K == 7 || K == 11) && dil >= 1 && dil <= 5;
+}
+
+// the bf16 scheme's 128-channel kernel-7 / 11 ResBlock1 iterations as pairs (direct convs, xt in LDS)
+// instead of two Winograd launches each; TTS_MI355X_PAIR128=0 keeps the Winograd convs (A/B)
+bool resblock_pair128(int mode, int C, int K) {
+  const char* e = std::getenv("TTS_MI355X_PAIR128");
+  return mode == MATH_BF16 && C == 128 && (K == 7 || K == 11) && !(e && e[0] == '0');
 }
 
 // Where the fused form is the faster one (MI355X A/B, f16x3): every 32-channel iteration

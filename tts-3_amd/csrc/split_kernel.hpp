@@ -104,7 +104,8 @@ __device__ __forceinline__ void gate_epilogue(const Conv1dArgs& args, const f32x
 #define SPLIT_W_B1 3  // waves per SIMD asked of the bf16 scheme's split conv kernels (0: no request; 3: k3 c256 1.23 -> 1.05 ms, ups x2 -13%; 4 spills)
 #endif
 template <class S, int K, int BM, int BN, int TM, int TN, int G, int HMAX, int PD, bool GATE = false, int PL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S::NP == 1 && SPLIT_W_B1 > 0 ? SPLIT_W_B1 : 1)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S::NP == 1 && SPLIT_W_B1 > 0 && !(TN == 4 && HMAX == 96)
+                                                                          ? SPLIT_W_B1 : 1)))
 void conv1d_split_kernel(Conv1dArgs a) {
   using C = SplitCfg<S, K, BM, BN, TM, TN, G, HMAX, PD>;
   constexpr int NP = S::NP;
