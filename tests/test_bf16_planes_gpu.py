@@ -153,5 +153,26 @@ def test_bf16_pair128_matches_winograd(cuda_device, monkeypatch, planes):
         pairs = [n for n in names if n.startswith("mrf_pair_k") and n.endswith("_c128")]
         winos = [n for n in names if n.startswith("mrf_wino_k") and n.endswith("_c128")]
         assert (len(pairs), len(winos)) == ((6, 0) if p128 == "1" else (0, 12)), names
+        # the 256-channel kernel-3 / 7 iterations run as pairs in both arms (TTS_MI355X_PAIR256)
+        assert sum(n.startswith("mrf_pair_k") and n.endswith("_c256") for n in names) == 6, names
         assert_close_fp32(outs[p128], ref, f"pair128={p128} planes={planes}", **tol("bf16"))
+    assert max_abs(outs["1"].numpy(), outs["0"].numpy()) <= 2 * tol("bf16")["max_abs_tol"]
+
+
+def test_bf16_pair256_matches_per_conv(cuda_device, monkeypatch):
+    """bf16: the 256-channel kernel-3 / 7 ResBlock1 iterations as fused pairs on 128-column tiles
+    against their per-conv launches (TTS_MI355X_PAIR256=0: Winograd k7, direct k3), over several
+    tiles per utterance and a ragged tail."""
+    sd = synthetic.hifigan_state_dict(seed=67, weight_norm=False)
+    mel = synthetic.mel(2, 53, seed=11)
+    ref = hifigan_ref.hifigan_forward(sd, mel, pad=5, dtype=torch.float64, **V1)
+    outs = {}
+    for p256 in ("1", "0"):
+        monkeypatch.setenv("TTS_MI355X_PAIR256", p256)
+        g = _gen(V1, sd, cuda_device)
+        outs[p256] = g.inference(mel.to(cuda_device)).cpu()
+        names = [r["name"] for r in g.profile(mel.to(cuda_device))[1]]
+        n256 = sum(n.startswith("mrf_pair_k") and n.endswith("_c256") for n in names)
+        assert n256 == (6 if p256 == "1" else 0), names
+        assert_close_fp32(outs[p256], ref, f"pair256={p256}", **tol("bf16"))
     assert max_abs(outs["1"].numpy(), outs["0"].numpy()) <= 2 * tol("bf16")["max_abs_tol"]

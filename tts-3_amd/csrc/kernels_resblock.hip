@@ -73,7 +73,7 @@ struct PairCfg {
 #endif
 template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false, int PL = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    S::NP == 1 && PAIR_W_B1 > 0 && C <= 64 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1))))
+    C > 64 ? 1 : (S::NP == 1 && PAIR_W_B1 > 0 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))))
 void resblock_pair_kernel(ResPairArgs pa) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;
@@ -459,6 +459,12 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
       launch_pair_t<S, K, 128, 0>(a, B, s);
       return;
     }
+    // 256 channels on 128 columns (2 x 2 waves of 128 rows x 64 columns): xt 16 groups x 160 rows
+    // x 48 B = 123 KB
+    if (C == 256) {
+      launch_pair_t<S, K, 256, 2>(a, B, s);
+      return;
+    }
   }
   if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
   else if (C == 64 && pair_geo64() == 2 && S::ROWB <= 80) launch_pair_t<S, K, 64, 2>(a, B, s);
@@ -478,15 +484,22 @@ void launch_pair_s(const ResPairArgs& a, int B, int K, int C, hipStream_t s) {
 }  // namespace
 
 bool resblock_pair_supported(int mode, int C, int K, int dil) {
-  return is_split_mode(mode) && (C == 32 || C == 64 || (C == 128 && mode == MATH_BF16)) &&
+  return is_split_mode(mode) && (C == 32 || C == 64 || ((C == 128 || C == 256) && mode == MATH_BF16)) &&
          (K == 3 || K == 7 || K == 11) && dil >= 1 && dil <= 5;
 }
 
-// the bf16 scheme's 128-channel kernel-7 / 11 ResBlock1 iterations as pairs (direct convs, xt in LDS)
-// instead of two Winograd launches each; TTS_MI355X_PAIR128=0 keeps the Winograd convs (A/B)
+// the bf16 scheme's wide ResBlock1 iterations as pairs (direct convs, xt in LDS): 128 channels at
+// kernels 7 / 11 (instead of two Winograd launches each; TTS_MI355X_PAIR128=0 keeps those) and 256
+// channels at kernels 3 / 7 (TTS_MI355X_PAIR256=0 keeps the per-conv launches).  Measured per bf16
+// forward (profiles/ab_r06_bf16_pair128.txt, ab_r06_bf16_pair256.txt): c128 k11 5.44 -> 4.98 ms,
+// k7 4.95 -> 3.93; c256 k7 2.04 -> 1.69, k3 1.05 -> 0.99, k11 2.43 -> 2.63 (stays Winograd)
 bool resblock_pair128(int mode, int C, int K) {
-  const char* e = std::getenv("TTS_MI355X_PAIR128");
-  return mode == MATH_BF16 && C == 128 && (K == 7 || K == 11) && !(e && e[0] == '0');
+  if (mode != MATH_BF16) return false;
+  const char* e128 = std::getenv("TTS_MI355X_PAIR128");
+  const char* e256 = std::getenv("TTS_MI355X_PAIR256");
+  if (C == 128) return (K == 7 || K == 11) && !(e128 && e128[0] == '0');
+  if (C == 256) return (K == 3 || K == 7) && !(e256 && e256[0] == '0');
+  return false;
 }
 
 // Where the fused form is the faster one (MI355X A/B, f16x3): every 32-channel iteration
