@@ -66,9 +66,12 @@ extern "C" {
  *                     HiFiGAN executor runs conv_pre (user input, no statistics) in FP32_X6.
  *                     HiFiGAN, the Glow decoder and the VITS flow; the Glow encoder rejects it
  *                     (TTS_ERR_UNSUPPORTED).
- *   TTS_MATH_BF16     bf16 operands on v_mfma_f32_32x32x16_bf16 with fp32 accumulation and fp32
- *                     activations in HBM (the bf16 arithmetic of configs 3 / 5; not fp32-faithful:
- *                     ~2^-9 relative per product). */
+ *   TTS_MATH_BF16     bf16 operands on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the bf16
+ *                     arithmetic of configs 3 / 5; not fp32-faithful: ~2^-9 relative per product).
+ *                     The HiFiGAN executor keeps its internal activation planes in HBM as bf16 (one
+ *                     rounding per stored plane, as a bf16 PyTorch forward has; the environment
+ *                     variable TTS_MI355X_BF16_PLANES=0 at create time keeps them fp32); every tensor
+ *                     crossing this ABI stays fp32. */
 #define TTS_MATH_FP32 0
 #define TTS_MATH_FP32_X6 1
 #define TTS_MATH_FP32_F16X3 2

@@ -456,7 +456,13 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
     // accumulators per wave), the xt buffer 8 groups x 288 rows x 48 B = 111 KB (the 16-bit-pair
     // schemes' 80-byte rows would need 184 KB)
     if (C == 128) {
-      launch_pair_t<S, K, 128, 0>(a, B, s);
+      // TTS_MI355X_PAIR128_GEO=2 (A/B): 128 columns, 2 x 2 waves of 64 x 64, 78 KB (two per CU)
+      static const int geo = [] {
+        const char* e = std::getenv("TTS_MI355X_PAIR128_GEO");
+        return e && e[0] == '2' ? 2 : 0;
+      }();
+      if (geo == 2) launch_pair_t<S, K, 128, 2>(a, B, s);
+      else launch_pair_t<S, K, 128, 0>(a, B, s);
       return;
     }
     // 256 channels on 128 columns (2 x 2 waves of 128 rows x 64 columns): xt 16 groups x 160 rows
