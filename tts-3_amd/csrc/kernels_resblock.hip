@@ -30,6 +30,9 @@ namespace tts {
 //   GEO 1 (C = 64): RP_W = 192, waves 2 x 2, each 32 rows x 96 columns: the xt buffer shrinks
 //   from 4 x 288 to 4 x 224 rows, so two workgroups fit a CU in the f16x3 scheme (LDS 72 KB
 //   instead of 92 KB); the halo costs (K - 1) / 192 of the columns instead of (K - 1) / 256.
+//   GEO 4 (bf16 C = 128, A/B TTS_MI355X_PAIR128_GEO=4): RP_W = 256, waves 2 x 2 of 64 x 128: a
+//   weight fragment feeds 4 MFMAs instead of GEO 0's 2 (GEO 0 at C = 128 streams 64 B/clk of
+//   weights per CU at full MFMA rate, the L2 port's width).
 //   GEO 2 (C = 64, round 6 A/B, TTS_MI355X_PAIR_GEO64=2): RP_W = 128, waves 2 x 2 of 32 x 64,
 //   double-buffered staging: 51 KB of LDS and <= 168 VGPRs, three workgroups (three waves per
 //   SIMD) per CU.
@@ -39,10 +42,10 @@ constexpr int kPostHalo = 3;  // its zero-padding halo per side
 
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
-  static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_W = (GEO == 0 || GEO == 4) ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
   static constexpr int RP_BN = RP_W - 2 * LEAD;
-  static constexpr int WN = GEO == 0 ? 4 : 2;
+  static constexpr int WN = GEO == 0 ? 4 : 2;  // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128)
   static constexpr int WM = 4 / WN;
   static constexpr int TM = C / 32 / WM;
   static constexpr int TN = RP_W / 32 / WN;
@@ -444,7 +447,7 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
 int pair_geo64() {
   static const int g = [] {
     const char* e = std::getenv("TTS_MI355X_PAIR_GEO64");
-    return e && std::atoi(e) == 2 ? 2 : 1;
+    return e && std::atoi(e) == 2 ? 2 : (e && std::atoi(e) == 4 ? 4 : 1);
   }();
   return g;
 }
@@ -456,12 +459,15 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
     // accumulators per wave), the xt buffer 8 groups x 288 rows x 48 B = 111 KB (the 16-bit-pair
     // schemes' 80-byte rows would need 184 KB)
     if (C == 128) {
-      // TTS_MI355X_PAIR128_GEO=2 (A/B): 128 columns, 2 x 2 waves of 64 x 64, 78 KB (two per CU)
+      // default GEO 4 (256 columns, 2 x 2 waves of 64 x 128: step 26.41 -> 26.2 ms,
+      // profiles/ab_r06_bf16_pair128_geo.txt); TTS_MI355X_PAIR128_GEO=0 (4 waves of 128 x 64) or 2
+      // (128 columns, 2 x 2 waves of 64 x 64, 78 KB: two per CU) for A/B
       static const int geo = [] {
         const char* e = std::getenv("TTS_MI355X_PAIR128_GEO");
-        return e && e[0] == '2' ? 2 : 0;
+        return e && e[0] == '2' ? 2 : (e && e[0] == '0' ? 0 : 4);
       }();
       if (geo == 2) launch_pair_t<S, K, 128, 2>(a, B, s);
+      else if (geo == 4) launch_pair_t<S, K, 128, 4>(a, B, s);
       else launch_pair_t<S, K, 128, 0>(a, B, s);
       return;
     }
@@ -474,6 +480,7 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
   }
   if (C == 32) launch_pair_t<S, K, 32, 0>(a, B, s);
   else if (C == 64 && pair_geo64() == 2 && S::ROWB <= 80) launch_pair_t<S, K, 64, 2>(a, B, s);
+  else if (C == 64 && pair_geo64() == 4 && S::NP == 1) launch_pair_t<S, K, 64, 4>(a, B, s);
   else if (C == 64) launch_pair_t<S, K, 64, 1>(a, B, s);
   else throw Error(3, "resblock pair: channels must be 32 or 64");
 }
