@@ -127,6 +127,23 @@ __device__ __forceinline__ void lds_dma_b128(const void* base, unsigned bytes, u
 #pragma clang diagnostic pop
 }
 
+// L2 prefetch of one 4-byte element per lane through the LDS-DMA path: the line lands in L2 on
+// its way to a scratch LDS area (256 bytes at lds), and no VGPR is written, so nothing has to stay
+// live until the load returns.  Later vmcnt waits of the issuing wave count it (in order).
+__device__ __forceinline__ void l2_touch_dma(const void* base, unsigned bytes, unsigned voff, const void* lds) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  const u32x4_t d = {(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
+                     (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)),
+                     (unsigned)__builtin_amdgcn_readfirstlane((int)act_range(bytes)), 0x00020000u};
+  const unsigned m =
+      (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(unsigned long)(__attribute__((address_space(3))) const void*)lds);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(d), "s"(m)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
 // leaky_relu for 0 < slope <= 1 (slope 1 = identity): max(x, slope*x), 2 VALU
 __device__ __forceinline__ float lrelu2(float x, float slope) { return fmaxf(x, x * slope); }
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }

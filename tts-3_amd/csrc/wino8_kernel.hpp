@@ -441,6 +441,34 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   if (grp == 0) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
 
+#ifndef WINO8_EPI_PF
+#define WINO8_EPI_PF 0
+#endif
+  // L2 prefetch of the epilogue's gathers (dilation 1: the residual and the MRF sum): every
+  // 128-byte line of this workgroup's 128-row x TW-sample output tile is touched once, right after
+  // the wave's last weight load, so the gathers after the output transform and the partial-sum
+  // exchange hit L2 instead of HBM.  The LDS-DMA writes land in the raw windows, which nothing
+  // reads after the last chunk's transform (the chunk before it)
+  if constexpr (WINO8_EPI_PF && D == 1) {
+    if (a.res || a.zmode >= 2) {
+      constexpr unsigned YES = PlaneT<YB>::ES;
+      constexpr int LPR = C::TW * (int)YES / 128;  // lines per row
+      const unsigned plane = (unsigned)a.Cout * (unsigned)a.Tout * YES;
+      const size_t item = (size_t)b * (a.o_bstride ? a.o_bstride : (int64_t)a.Cout * a.Tout);
+      const void* pres = a.res ? plane_at<YB>(a.res, item) : nullptr;
+      const void* pz = a.zmode >= 2 ? plane_at<YB>(a.z, item) : nullptr;
+#pragma unroll
+      for (int i = 0; i < (128 * LPR + 511) / 512; ++i) {
+        const int l = tid + 512 * i;
+        const int co = mt * 128 + l / LPR, ln = l % LPR;
+        const int t = t0 + ln * (128 / (int)YES);
+        const unsigned vo = (l < 128 * LPR && co < a.Cout && t < a.Tout) ? ((unsigned)co * (unsigned)a.Tout + (unsigned)t) * YES : OOB_OFF;
+        if (pres) l2_touch_dma(pres, plane, vo, rsm);
+        if (pz) l2_touch_dma(pz, plane, vo, rsm + 256);
+      }
+    }
+  }
+
   // ---- epilogue ----
   if (WINO_ABLATE & 16) {
     float sum = 0.f;
