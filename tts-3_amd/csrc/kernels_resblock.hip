@@ -36,17 +36,24 @@ namespace tts {
 //   GEO 2 (C = 64, round 6 A/B, TTS_MI355X_PAIR_GEO64=2): RP_W = 128, waves 2 x 2 of 32 x 64,
 //   double-buffered staging: 51 KB of LDS and <= 168 VGPRs, three workgroups (three waves per
 //   SIMD) per CU.
+//   GEO 5 / 6 (bf16 C = 128 / 256, the defaults there): 8 waves, two per SIMD, each 64 rows x 64
+//   columns; 2 x 4 waves on 256 columns (C = 128) or 4 x 2 on 128 (C = 256).  The xt buffer keeps
+//   the workgroup alone on its CU, so the second wave per SIMD is what hides one wave's staging,
+//   hand-off and epilogue latencies.
 
 constexpr int kPostK = 7;     // conv_post kernel (hifigan_generator.py:229-230)
 constexpr int kPostHalo = 3;  // its zero-padding halo per side
 
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
-  static constexpr int RP_W = (GEO == 0 || GEO == 4) ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_W = (GEO == 0 || GEO == 4 || GEO == 5) ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
   static constexpr int RP_BN = RP_W - 2 * LEAD;
-  static constexpr int WN = GEO == 0 ? 4 : 2;  // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128)
-  static constexpr int WM = 4 / WN;
+  static constexpr int NW = GEO >= 5 ? 8 : 4;     // waves per workgroup
+  static constexpr int NT = 64 * NW;
+  // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128); GEO 5 / 6: 8 waves, 2 x 4 / 4 x 2
+  static constexpr int WN = (GEO == 0 || GEO == 5) ? 4 : 2;
+  static constexpr int WM = NW / WN;
   static constexpr int TM = C / 32 / WM;
   static constexpr int TN = RP_W / 32 / WN;
   static constexpr int NC = C / 16;               // 16-channel groups
@@ -64,7 +71,7 @@ struct PairCfg {
   static constexpr int LDSB = LDSB0 > ZTB ? LDSB0 : ZTB;
   // POST: output tiles overlap by conv_post's halo on both sides
   static constexpr int STRIDE = POST ? RP_BN - 2 * kPostHalo : RP_BN;
-  static constexpr int UPT = (XROWS * 4 + 255) / 256;
+  static constexpr int UPT = (XROWS * 4 + NT - 1) / NT;
   static_assert(TM >= 1 && TM * WM * 32 == C && TN * WN * 32 == RP_W, "geometry");
 };
 
@@ -75,8 +82,8 @@ struct PairCfg {
 #define PAIR_W_B1 3  // waves per SIMD asked of the bf16 scheme's pair kernels (0: as the others; 3 measured -1% per bf16 step, profiles/ab_r06_bf16_occupancy.txt)
 #endif
 template <class S, int K, int C, int PD, int GEO, bool ALLX, bool POST = false, int PL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    C > 64 ? 1 : (S::NP == 1 && PAIR_W_B1 > 0 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))))
+__global__ __launch_bounds__((PairCfg<S, K, C, PD, GEO, ALLX, POST>::NT)) __attribute__((amdgpu_waves_per_eu(
+    C > 64 ? (GEO >= 5 ? 2 : 1) : (S::NP == 1 && PAIR_W_B1 > 0 ? PAIR_W_B1 : ((C == 32 || GEO == 2) && S::ROWB <= 80 ? 3 : 1)))))
 void resblock_pair_kernel(ResPairArgs pa) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;
@@ -87,7 +94,8 @@ void resblock_pair_kernel(ResPairArgs pa) {
   constexpr bool H3 = S::SCALED;
   constexpr int TM = P::TM, TN = P::TN, NC = P::NC;
   __shared__ __attribute__((aligned(16))) unsigned char smem[P::LDSB];
-  __shared__ float red[4];
+  __shared__ float red[P::NW];
+  constexpr int NT = P::NT;
   __shared__ float bsm[2 * C];  // convs1 and convs2 biases (epilogue reads from LDS, not L2)
   __shared__ float pws[POST ? C * kPostK : 1];  // POST: conv_post's weights (broadcast reads)
 
@@ -180,7 +188,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
   int ulds[P::UPT];
 #pragma unroll
   for (int i = 0; i < P::UPT; ++i) {
-    const int u = tid + i * 256;
+    const int u = tid + i * NT;
     // RES_STAGE_8R: 8 rows x 2 quad positions per 16-lane store group (see conv1d_split_kernel)
     const int q = RES_STAGE_8R ? quad_pos((u >> 3) & 3) : (u & 3);
     const int r = RES_STAGE_8R ? (u >> 5) * 8 + (u & 7) : (u >> 2);
@@ -273,7 +281,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
     bsm[C + tid] = bias2;
   }
   if constexpr (POST)
-    for (int e = tid; e < C * kPostK; e += 256) pws[e] = pa.post_w[e];
+    for (int e = tid; e < C * kPostK; e += NT) pws[e] = pa.post_w[e];
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -329,7 +337,9 @@ void resblock_pair_kernel(ResPairArgs pa) {
       tmax = wave_max(tmax);
       if (lane == 0) red[wave] = tmax;
       __syncthreads();
-      const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      float mx = red[0];
+#pragma unroll
+      for (int w = 1; w < P::NW; ++w) mx = fmaxf(mx, red[w]);
       if (mx > 0.f && mx < INFINITY) {
         int E;
         (void)frexpf(mx, &E);
@@ -349,7 +359,7 @@ void resblock_pair_kernel(ResPairArgs pa) {
                        acc[m][n], 8 * gl, tscale);
     // zero rows RP_W .. TROWS-1 of every group (read only by the discarded columns)
     constexpr int ZB = (P::TROWS - RP_W) * S::ROWB;  // bytes per group
-    for (int e = tid * 16; e < NC * ZB; e += 256 * 16) {
+    for (int e = tid * 16; e < NC * ZB; e += NT * 16) {
       const int g = e / ZB;
       *reinterpret_cast<f32x4*>(smem + (g * P::TROWS + RP_W) * S::ROWB + (e - g * ZB)) = f32x4{};
     }
@@ -427,11 +437,12 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
       using P = PairCfg<S, K, C, PD, GEO, AX, true>;
       static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
       dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
-      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, true, PL>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, true, PL>), grid, dim3(P::NT), 0, s, a);
       return;
     }
-    dim3 grid(ceil_div(a.c1.Tout, PairCfg<S, K, C, PD, GEO>::RP_BN), 1, B);
-    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, false, PL>), grid, dim3(256), 0, s, a);
+    using P = PairCfg<S, K, C, PD, GEO, AX>;
+    dim3 grid(ceil_div(a.c1.Tout, P::RP_BN), 1, B);
+    hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, false, PL>), grid, dim3(P::NT), 0, s, a);
   };
   if (a.c1.planes != 0) {
     // bf16 activation planes: x, x' and z all bf16 (the bf16 scheme)
@@ -459,22 +470,32 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
     // accumulators per wave), the xt buffer 8 groups x 288 rows x 48 B = 111 KB (the 16-bit-pair
     // schemes' 80-byte rows would need 184 KB)
     if (C == 128) {
-      // default GEO 4 (256 columns, 2 x 2 waves of 64 x 128: step 26.41 -> 26.2 ms,
-      // profiles/ab_r06_bf16_pair128_geo.txt); TTS_MI355X_PAIR128_GEO=0 (4 waves of 128 x 64) or 2
-      // (128 columns, 2 x 2 waves of 64 x 64, 78 KB: two per CU) for A/B
+      // default GEO 5 (256 columns, 8 waves of 64 x 64, two per SIMD: k7 3.79 -> 3.59 ms, k11
+      // 4.89 -> 4.80 per forward, profiles/ab_r06_bf16_pair8w.txt); TTS_MI355X_PAIR128_GEO=4 (2 x 2
+      // waves of 64 x 128, one per SIMD: step 26.41 -> 26.2 ms against GEO 0,
+      // profiles/ab_r06_bf16_pair128_geo.txt), 0 (4 waves of 128 x 64) or 2 (128 columns, 2 x 2 waves
+      // of 64 x 64, 78 KB: two per CU) for A/B
       static const int geo = [] {
         const char* e = std::getenv("TTS_MI355X_PAIR128_GEO");
-        return e && e[0] == '2' ? 2 : (e && e[0] == '0' ? 0 : 4);
+        return e && e[0] == '2' ? 2 : (e && e[0] == '0' ? 0 : (e && e[0] == '4' ? 4 : 5));
       }();
       if (geo == 2) launch_pair_t<S, K, 128, 2>(a, B, s);
+      else if (geo == 5) launch_pair_t<S, K, 128, 5>(a, B, s);
       else if (geo == 4) launch_pair_t<S, K, 128, 4>(a, B, s);
       else launch_pair_t<S, K, 128, 0>(a, B, s);
       return;
     }
-    // 256 channels on 128 columns (2 x 2 waves of 128 rows x 64 columns): xt 16 groups x 160 rows
-    // x 48 B = 123 KB
+    // 256 channels on 128 columns: xt 16 groups x 160 rows x 48 B = 123 KB
     if (C == 256) {
-      launch_pair_t<S, K, 256, 2>(a, B, s);
+      // default GEO 6: 8 waves of 64 rows x 64 columns, two per SIMD (k7 1.80 -> 1.63 ms, k3 0.99 ->
+      // 0.91 per forward, profiles/ab_r06_bf16_pair8w.txt); TTS_MI355X_PAIR256_GEO=2 keeps 2 x 2 waves
+      // of 128 x 64, one per SIMD
+      static const int geo = [] {
+        const char* e = std::getenv("TTS_MI355X_PAIR256_GEO");
+        return e && e[0] == '2' ? 2 : 6;
+      }();
+      if (geo == 6) launch_pair_t<S, K, 256, 6>(a, B, s);
+      else launch_pair_t<S, K, 256, 2>(a, B, s);
       return;
     }
   }
