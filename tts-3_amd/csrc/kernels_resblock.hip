@@ -532,7 +532,11 @@ bool resblock_pair128(int mode, int C, int K) {
   const char* e128 = std::getenv("TTS_MI355X_PAIR128");
   const char* e256 = std::getenv("TTS_MI355X_PAIR256");
   if (C == 128) return (K == 7 || K == 11) && !(e128 && e128[0] == '0');
-  if (C == 256) return (K == 3 || K == 7) && !(e256 && e256[0] == '0');
+  if (C == 256) {
+    // kernel 11 at 256 channels: Winograd unless TTS_MI355X_PAIR256_K11=1 (A/B)
+    const char* e11 = std::getenv("TTS_MI355X_PAIR256_K11");
+    return (K == 3 || K == 7 || (K == 11 && e11 && e11[0] == '1')) && !(e256 && e256[0] == '0');
+  }
   return false;
 }
 
