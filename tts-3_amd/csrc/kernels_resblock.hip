@@ -36,23 +36,25 @@ namespace tts {
 //   GEO 2 (C = 64, round 6 A/B, TTS_MI355X_PAIR_GEO64=2): RP_W = 128, waves 2 x 2 of 32 x 64,
 //   double-buffered staging: 51 KB of LDS and <= 168 VGPRs, three workgroups (three waves per
 //   SIMD) per CU.
-//   GEO 5 / 6 (bf16 C = 128 / 256, the defaults there): 8 waves, two per SIMD, each 64 rows x 64
-//   columns; 2 x 4 waves on 256 columns (C = 128) or 4 x 2 on 128 (C = 256).  The xt buffer keeps
-//   the workgroup alone on its CU, so the second wave per SIMD is what hides one wave's staging,
-//   hand-off and epilogue latencies.
+//   GEO 5 / 6 (bf16 C = 128 / 256): 8 waves, two per SIMD, each 64 rows x 64 columns; 2 x 4 waves
+//   on 256 columns (C = 128) or 4 x 2 on 128 (C = 256).  The xt buffer keeps the workgroup alone
+//   on its CU, so the second wave per SIMD is what hides one wave's staging, hand-off and epilogue
+//   latencies.  GEO 7 / 8 (the bf16 defaults): the same with waves of 32 rows x 128 columns (4 x 2
+//   on 256 columns, 8 x 1 on 128), so a weight fragment feeds 4 MFMAs.
 
 constexpr int kPostK = 7;     // conv_post kernel (hifigan_generator.py:229-230)
 constexpr int kPostHalo = 3;  // its zero-padding halo per side
 
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
-  static constexpr int RP_W = (GEO == 0 || GEO == 4 || GEO == 5) ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_W = (GEO == 0 || GEO == 4 || GEO == 5 || GEO == 7) ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
   static constexpr int RP_BN = RP_W - 2 * LEAD;
   static constexpr int NW = GEO >= 5 ? 8 : 4;     // waves per workgroup
   static constexpr int NT = 64 * NW;
-  // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128); GEO 5 / 6: 8 waves, 2 x 4 / 4 x 2
-  static constexpr int WN = (GEO == 0 || GEO == 5) ? 4 : 2;
+  // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128); GEO 5 / 6: 8 waves, 2 x 4 / 4 x 2; GEO 7 / 8
+  // (A/B): 8 waves of 32 rows x 128 columns, 4 x 2 / 8 x 1 (a weight fragment feeds 4 MFMAs)
+  static constexpr int WN = (GEO == 0 || GEO == 5) ? 4 : (GEO == 8 ? 1 : 2);
   static constexpr int WM = NW / WN;
   static constexpr int TM = C / 32 / WM;
   static constexpr int TN = RP_W / 32 / WN;
@@ -470,16 +472,19 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
     // accumulators per wave), the xt buffer 8 groups x 288 rows x 48 B = 111 KB (the 16-bit-pair
     // schemes' 80-byte rows would need 184 KB)
     if (C == 128) {
-      // default GEO 5 (256 columns, 8 waves of 64 x 64, two per SIMD: k7 3.79 -> 3.59 ms, k11
-      // 4.89 -> 4.80 per forward, profiles/ab_r06_bf16_pair8w.txt); TTS_MI355X_PAIR128_GEO=4 (2 x 2
+      // default GEO 7 (256 columns, 8 waves of 32 x 128, two per SIMD, a weight fragment feeding 4
+      // MFMAs: step -0.2 ms against GEO 5, profiles/ab_r06_bf16_pair78.txt); TTS_MI355X_PAIR128_GEO=5
+      // (8 waves of 64 x 64: k7 3.79 -> 3.59 ms, k11 4.89 -> 4.80 per forward against GEO 4,
+      // profiles/ab_r06_bf16_pair8w.txt), 4 (2 x 2
       // waves of 64 x 128, one per SIMD: step 26.41 -> 26.2 ms against GEO 0,
       // profiles/ab_r06_bf16_pair128_geo.txt), 0 (4 waves of 128 x 64) or 2 (128 columns, 2 x 2 waves
       // of 64 x 64, 78 KB: two per CU) for A/B
       static const int geo = [] {
         const char* e = std::getenv("TTS_MI355X_PAIR128_GEO");
-        return e && e[0] == '2' ? 2 : (e && e[0] == '0' ? 0 : (e && e[0] == '4' ? 4 : 5));
+        return e && e[0] == '2' ? 2 : (e && e[0] == '0' ? 0 : (e && e[0] == '4' ? 4 : (e && e[0] == '5' ? 5 : 7)));
       }();
       if (geo == 2) launch_pair_t<S, K, 128, 2>(a, B, s);
+      else if (geo == 7) launch_pair_t<S, K, 128, 7>(a, B, s);
       else if (geo == 5) launch_pair_t<S, K, 128, 5>(a, B, s);
       else if (geo == 4) launch_pair_t<S, K, 128, 4>(a, B, s);
       else launch_pair_t<S, K, 128, 0>(a, B, s);
@@ -487,14 +492,16 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
     }
     // 256 channels on 128 columns: xt 16 groups x 160 rows x 48 B = 123 KB
     if (C == 256) {
-      // default GEO 6: 8 waves of 64 rows x 64 columns, two per SIMD (k7 1.80 -> 1.63 ms, k3 0.99 ->
-      // 0.91 per forward, profiles/ab_r06_bf16_pair8w.txt); TTS_MI355X_PAIR256_GEO=2 keeps 2 x 2 waves
-      // of 128 x 64, one per SIMD
+      // default GEO 8: 8 waves of 32 rows x 128 columns, two per SIMD (k3 0.91 -> 0.86 ms per forward
+      // against GEO 6, profiles/ab_r06_bf16_pair78.txt); TTS_MI355X_PAIR256_GEO=6 (8 waves of 64 x 64:
+      // k7 1.80 -> 1.63 ms, k3 0.99 -> 0.91 against GEO 2, profiles/ab_r06_bf16_pair8w.txt) or 2
+      // (2 x 2 waves of 128 x 64, one per SIMD)
       static const int geo = [] {
         const char* e = std::getenv("TTS_MI355X_PAIR256_GEO");
-        return e && e[0] == '2' ? 2 : 6;
+        return e && e[0] == '2' ? 2 : (e && e[0] == '6' ? 6 : 8);
       }();
       if (geo == 6) launch_pair_t<S, K, 256, 6>(a, B, s);
+      else if (geo == 8) launch_pair_t<S, K, 256, 8>(a, B, s);
       else launch_pair_t<S, K, 256, 2>(a, B, s);
       return;
     }
