@@ -87,6 +87,13 @@ def main():
         algo = 4.0 * B * 80 * T
         calib = {"kernel": "amax_mel", "algorithmic_read_bytes": algo, "raw_fetch_bytes": per["FETCH_SIZE"]["amax_mel"]}
         fetch_scale = algo / per["FETCH_SIZE"]["amax_mel"]
+    else:
+        # no amax_mel launch (bf16 mode): the probe calibration of the same staging lane map
+        # (profiles/fetch_calibration_r06.txt: a 1,084,227,584-byte plane read once counts
+        # 529,419.5 KiB of FETCH_SIZE, exactly half)
+        fetch_scale = 1084227584.0 / (529419.5 * 1024.0)
+        calib = {"probe": "profiles/fetch_calibration_r06.txt (scripts/probe_fetch.hip, staging lane map)",
+                 "algorithmic_read_bytes": 1084227584.0, "raw_fetch_bytes": 529419.5 * 1024.0}
     fams = sorted(set(names), key=names.index)
     counts = {f: names.count(f) for f in fams}
     per_launch = {}
@@ -119,7 +126,8 @@ def main():
                   f"B={B}, T={T}; scripts/profile_round.sh + scripts/traffic_from_pmc.py",
         "note": "bytes = FETCH_SIZE*1024*fetch_scale + WRITE_SIZE*1024 per launch, averaged over the profiled "
                 "forwards; fetch_scale calibrated in-run on amax_mel (exact read size, same 4-B/lane buffer-load "
-                "pattern as the activation staging). FETCH counts L2->fabric requests, i.e. HBM plus "
+                "pattern as the activation staging), or from the staging-pattern probe where no amax_mel runs "
+                "(bf16). FETCH counts L2->fabric requests, i.e. HBM plus "
                 "Infinity-Cache hits.",
         "fetch_scale": fetch_scale,
         "fetch_calibration": calib,
