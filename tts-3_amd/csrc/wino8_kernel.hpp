@@ -298,9 +298,21 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   const rsrc_t ra = make_rsrc(a.w + ((size_t)mb * nc * C::NS) * (NP * 256), 0xFFFFFFFFu);
   const unsigned avoff = (unsigned)lane * 16u;
 
-  f32x16 acc[4][2];
+#ifndef WINO8_NOXCH
+#define WINO8_NOXCH 0
+#endif
+  // NX (A/B): each wave accumulates all 7 points of ONE 32-column block (wave w column block 0,
+  // wave w + 4 block 1, the same 32 rows and weight steps): no partial-sum exchange in the
+  // epilogue and equal MFMA work in both groups, for twice the weight loads per MFMA (the pair's
+  // two waves load the same addresses).  The per-accumulator MFMA sequence and the output
+  // transform's sums are those of the point split, so the results are bitwise the same.
+  constexpr bool NX = WINO8_NOXCH != 0;
+  constexpr int NA = NX ? 7 : 4, NB = NX ? 1 : 2;  // accumulators: points x column blocks
+  f32x16 acc[NA][NB];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = f32x16{};
+  for (int p = 0; p < NA; ++p)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[p][n] = f32x16{};
   WSTAMP(0);
 
   float bpre = 0.f;
@@ -344,15 +356,16 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 
   // the chunk loop of one point group (NPG points starting at P0); both groups run it with the
   // same barrier sequence
-  auto run = [&](auto npg_tag, auto p0_tag) {
+  auto run = [&](auto npg_tag, auto p0_tag, auto g1_tag) {
     constexpr int NPG = decltype(npg_tag)::value;
     constexpr int P0 = decltype(p0_tag)::value;
+    constexpr bool G1 = decltype(g1_tag)::value;  // the DMA-issuing group (waves 4-7)
     constexpr int NV = NPG * NCH;  // MFMA steps per chunk for this wave
     // weight prefetch depth: the DMA-issuing waves (P0 > 0, 96 accumulator registers) prefetch
     // further ahead, so the in-order wait for their input DMA falls PDG steps after its issue
     // the bf16 scheme's steps are a third as long (one product per MAC): its own depths (A/B)
-    constexpr int PD = NP == 1 ? (P0 > 0 ? WINO8_PD1_B1 : WINO8_PD_B1)
-                               : (P0 > 0 ? WINO8_PD1 : (K == 11 ? WINO8_PD11 : WINO8_PD));
+    constexpr int PD = NP == 1 ? (G1 ? WINO8_PD1_B1 : WINO8_PD_B1)
+                               : (G1 ? WINO8_PD1 : (K == 11 ? WINO8_PD11 : WINO8_PD));
     // steps between a transform piece's LDS reads and its math (no later than the next piece's
     // reads); measured per kernel size
     constexpr int GAP0 = K == 11 ? WINO8_GAP11 : WINO8_GAP7;
@@ -362,7 +375,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       // prefetches past the last chunk (never used) re-read step 0 instead of running off the array
       return ck2 < nc ? (unsigned)((ck2 * C::NS + (v2 / NPG) * 7 + P0 + v2 % NPG) * NP) * 1024u : 0u;
     };
-    f32x4 ar[PD + 1][NP], bcur[2][NP], bnext[2][NP];
+    f32x4 ar[PD + 1][NP], bcur[NB][NP], bnext[NB][NP];
 #pragma unroll
     for (int v = 0; v < PD; ++v)
 #pragma unroll
@@ -371,8 +384,8 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     auto read_b = [&](const unsigned char* tl, int v, f32x4 (*dst)[NP]) {
       const int p = P0 + v % NPG, c = v / NPG;
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const unsigned char* ptr = tl + p * C::PLANE + (n * 32 + l32 + c * D) * S::ROWB + 16 * half;
+      for (int n = 0; n < NB; ++n) {
+        const unsigned char* ptr = tl + p * C::PLANE + ((NX ? grp : n) * 32 + l32 + c * D) * S::ROWB + 16 * half;
 #pragma unroll
         for (int q = 0; q < NP; ++q) dst[n][q] = *reinterpret_cast<const f32x4*>(ptr + 32 * q);
       }
@@ -391,13 +404,13 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
                                         : bload4(ra, avoff, ((WINO_ABLATE & 64) ? 0u : aoff(ck, v + PD)) + (unsigned)q * 1024u);
         if (v + 1 < NV) read_b(tl, v + 1, bnext);
         // raw(ck+2) -> R[ck & 1] (raw(ck) is consumed), two DMA instructions per step
-        if ((WINO_ABLATE & 32) == 0 && P0 > 0 && ck + 2 < nc && v < 3) dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);
+        if ((WINO_ABLATE & 32) == 0 && G1 && ck + 2 < nc && v < 3) dma(ck + 2, tb, 2 * v, v == 2 ? 64 : 2 * v + 2);
         __builtin_amdgcn_sched_barrier(0);
         const int p = v % NPG;
 #pragma unroll
         for (int e = 0; e < S::NPROD; ++e)
 #pragma unroll
-          for (int n = 0; n < 2; ++n) {
+          for (int n = 0; n < NB; ++n) {
             if (WINO_ABLATE & 8) acc[p][n][e] += ar[0][S::PA[e]][0] * bcur[n][S::PB[e]][0];
             else acc[p][n] = S::mfma(ar[0][S::PA[e]], bcur[n][S::PB[e]], acc[p][n]);
           }
@@ -407,7 +420,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
           for (int q = 0; q < NP; ++q) ar[pp][q] = ar[pp + 1][q];
         if (v + 1 < NV) {
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
+          for (int n = 0; n < NB; ++n)
 #pragma unroll
             for (int q = 0; q < NP; ++q) bcur[n][q] = bnext[n][q];
         }
@@ -428,7 +441,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       // raw(ck+2) landed: at most the weight loads issued after the last DMA (steps 3.. of this chunk)
       // may still be in flight
       constexpr int NAFTER = (PD < NV - 3 ? PD : NV - 3) * NP;
-      if (P0 > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NAFTER) : "memory");
+      if (G1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NAFTER) : "memory");
       if (ck < 8) WSTAMP(4 + 2 * ck);
       lds_sync();
     }
@@ -438,8 +451,13 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
 #endif
   if (WINO8_PRIO == 1 && grp == 1) __builtin_amdgcn_s_setprio(1);
   if (WINO8_PRIO == 2 && grp == 0) __builtin_amdgcn_s_setprio(1);
-  if (grp == 0) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{});
-  else run(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
+  if constexpr (NX) {
+    if (grp == 0) run(std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, std::false_type{});
+    else run(std::integral_constant<int, 7>{}, std::integral_constant<int, 0>{}, std::true_type{});
+  } else {
+    if (grp == 0) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 0>{}, std::false_type{});
+    else run(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{}, std::true_type{});
+  }
 
 #ifndef WINO8_EPI_PF
 #define WINO8_EPI_PF 0
@@ -473,9 +491,9 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   if (WINO_ABLATE & 16) {
     float sum = 0.f;
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < NA; ++p)
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int r = 0; r < 16; ++r) sum += acc[p][n][r];
     if (sum == 1234.5f) a.y[threadIdx.x] = sum;
@@ -484,6 +502,23 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
   // the f16x3 rescale sc (an exact power of two) commutes with the output transform: applied once
   // per output in wino_apply instead of once per point here
   const float sc = H3 ? ldexpf(1.f, ex + a.w_exp) : 1.f;
+  const int nk = grp;  // the column block this wave finishes
+  float y[4][16];
+  if constexpr (NX) {
+    // all 7 points of column block nk in this wave: the point-split sums (points 0-3) + (4-6),
+    // formed exactly as the exchange below forms them
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float m0 = acc[0][0][r], m1 = acc[1][0][r], m2 = acc[2][0][r], m3 = acc[3][0][r];
+      const float m4 = acc[4][0][r], m5 = acc[5][0][r], m6 = acc[6][0][r];
+      const float s12 = m1 + m2, d12 = m1 - m2;
+      y[0][r] = ((m0 + s12) + m3) + (m4 + m5);
+      y[1][r] = fmaf(2.f, m3, d12) + fmaf(-2.f, m4, 0.5f * m5);
+      y[2][r] = fmaf(4.f, m3, s12) + fmaf(4.f, m4, 0.25f * m5);
+      y[3][r] = fmaf(8.f, m3, d12) + (fmaf(-8.f, m4, 0.125f * m5) + m6);
+    }
+    WSTAMP(20);
+  } else {
   // partial outputs of this wave's points: yp[n][i][r]
   float yp[2][4][16];
 #pragma unroll
@@ -507,8 +542,6 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
     }
   WSTAMP(20);
   // swap halves: group 0 finishes column block 0, group 1 block 1 (two passes of 8 rows per lane)
-  const int nk = grp;
-  float y[4][16];
   // [wm][grp][8 r][64 lanes] float4 (the 4 outputs i of one register r): one ds_write_b128 /
   // ds_read_b128 per r, lanes contiguous (conflict-free), 64 KiB
   f32x4* xch = reinterpret_cast<f32x4*>(tsm);
@@ -530,6 +563,7 @@ __global__ __launch_bounds__(512) void conv1d_wino8_kernel(Conv1dArgs a) {
       for (int i = 0; i < 4; ++i) y[i][8 * h + r] = (grp == 0 ? yp[0][i][8 * h + r] : yp[1][i][8 * h + r]) + other[i];
     }
     lds_sync();
+  }
   }
 
   WSTAMP(21);
