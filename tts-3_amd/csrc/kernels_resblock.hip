@@ -597,17 +597,6 @@ void launch_res3_s(const ResBlock3Args& a, int B, int C, int K, hipStream_t s) {
   }
   if (C == 32) launch_res3_t<S, 32, 0, 3>(a, B, s);
   else if (C == 128) {
-    // bf16: TTS_MI355X_RB3_GEO128=4 (A/B) takes 256-column tiles of 8 waves of 32 x 128
-    static const int geo = [] {
-      const char* e = std::getenv("TTS_MI355X_RB3_GEO128");
-      return e && e[0] == '4' ? 4 : 3;
-    }();
-    if constexpr (S::ROWB <= 48) {
-      if (geo == 4) {
-        launch_res3_t<S, 128, 4, 3>(a, B, s);
-        return;
-      }
-    }
     if constexpr (S::ROWB <= 80) launch_res3_t<S, 128, 3, 3>(a, B, s);
     else throw Error(3, "resblock3: 128 channels need a split scheme of at most 80-byte rows");
   } else launch_res3_t<S, 64, 2, 3>(a, B, s);

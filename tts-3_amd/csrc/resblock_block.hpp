@@ -48,16 +48,13 @@ constexpr int rb2_halo(int K) { return K == 3 ? 4 : (K == 5 ? 12 : (K == 7 ? 9 :
 
 // GEO 0: 256 columns, 4 waves side by side; GEO 1 / 2: 192 / 128 columns, 2 x 2 waves;
 // GEO 3: 128 columns, 8 waves (4 row blocks x 2 column halves at C = 128, two waves per SIMD).
-// GEO 4 (bf16 C = 128: its 48-byte rows fit 266 rows x 8 groups in 102 KB): 256 columns, 8 waves of
-// 32 rows x 128 columns: a weight fragment feeds 4 MFMAs and the 12-column lead costs 10% of the
-// columns instead of 23%.
 // Measured (f16x3, per batch): C = 128 GEO 3 5.0 ms vs GEO 2 5.5 ms; 8-wave forms at C = 64
 // (256 columns) and C = 32 (512 columns) were slower than GEO 2 / GEO 0 (+0.2 / +0.3 ms).
 template <class S, int C, int GEO, int K = 3, int NCV = 6, int XO = R3_XOFF, int LEAD = R3_LEAD>
 struct Res3Cfg {
-  static constexpr int RP_W = (GEO == 0 || GEO == 4) ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_W = GEO == 0 ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int RP_BN = RP_W - 2 * LEAD;
-  static constexpr int NW = (GEO == 3 || GEO == 4) ? 8 : 4;     // waves per workgroup
+  static constexpr int NW = GEO == 3 ? 8 : 4;     // waves per workgroup
   static constexpr int NT = 64 * NW;
   static constexpr int WN = GEO == 0 ? 4 : 2;
   static constexpr int WM = NW / WN;
@@ -79,7 +76,7 @@ struct Res3Cfg {
 template <class S, int C, int GEO, int K, int NCV, int XO, int LEAD, int PL = 0>
 __global__ __launch_bounds__((Res3Cfg<S, C, GEO, K, NCV, XO, LEAD>::NT))
 __attribute__((amdgpu_waves_per_eu(S::NP == 1 && RB3_W_B1 > 0 ? RB3_W_B1
-                                                                : (C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO >= 3 ? 2 : 1)))))
+                                                                : (C == 64 && GEO == 2 ? RB3_W64 : (C == 32 || GEO == 3 ? 2 : 1)))))
 void resblock3_kernel(ResBlock3Args a) {
   constexpr bool XB = (PL & kPlaneXB16) != 0, YB = (PL & kPlaneYB16) != 0;
   using PX = PlaneT<XB>;
