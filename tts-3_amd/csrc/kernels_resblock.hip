@@ -47,11 +47,10 @@ constexpr int kPostHalo = 3;  // its zero-padding halo per side
 
 template <class S, int K, int C, int PD, int GEO, bool ALLX = false, bool POST = false>
 struct PairCfg {
-  static constexpr int RP_W = (GEO == 0 || GEO == 4 || GEO == 5 || GEO == 7 || GEO == 9) ? 256 : (GEO == 1 ? 192 : 128);
+  static constexpr int RP_W = (GEO == 0 || GEO == 4 || GEO == 5 || GEO == 7) ? 256 : (GEO == 1 ? 192 : 128);
   static constexpr int LEAD = (K - 1) / 2;        // xt row 0 holds time t0 - LEAD (conv2's halo)
   static constexpr int RP_BN = RP_W - 2 * LEAD;
-  // waves per workgroup (GEO 9, bf16 C = 32 A/B: 2 waves of 32 x 128, a weight fragment feeds 4 MFMAs)
-  static constexpr int NW = GEO == 9 ? 2 : (GEO >= 5 ? 8 : 4);
+  static constexpr int NW = GEO >= 5 ? 8 : 4;     // waves per workgroup
   static constexpr int NT = 64 * NW;
   // GEO 4: 256 columns as 2 x 2 waves (bf16 C = 128); GEO 5 / 6: 8 waves, 2 x 4 / 4 x 2; GEO 7 / 8
   // (A/B): 8 waves of 32 rows x 128 columns, 4 x 2 / 8 x 1 (a weight fragment feeds 4 MFMAs)
@@ -437,11 +436,10 @@ void launch_pair_t(const ResPairArgs& a, int B, hipStream_t s) {
   auto go = [&](auto pl_tag) {
     constexpr int PL = decltype(pl_tag)::value;
     if (a.post_w) {
-      constexpr int GP = GEO == 9 ? 0 : GEO;  // the fused conv_post needs a thread per column
-      using P = PairCfg<S, K, C, PD, GP, AX, true>;
-      static_assert(P::RP_BN - 2 * kPostHalo <= P::NT, "one conv_post column per thread");
+      using P = PairCfg<S, K, C, PD, GEO, AX, true>;
+      static_assert(P::RP_BN - 2 * kPostHalo <= 256, "one conv_post column per thread");
       dim3 grid(ceil_div(a.c1.Tout, P::STRIDE), 1, B);
-      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GP, AX, true, PL>), grid, dim3(P::NT), 0, s, a);
+      hipLaunchKernelGGL((resblock_pair_kernel<S, K, C, PD, GEO, AX, true, PL>), grid, dim3(P::NT), 0, s, a);
       return;
     }
     using P = PairCfg<S, K, C, PD, GEO, AX>;
@@ -505,17 +503,6 @@ void launch_pair_k(const ResPairArgs& a, int B, int C, hipStream_t s) {
       if (geo == 6) launch_pair_t<S, K, 256, 6>(a, B, s);
       else if (geo == 8) launch_pair_t<S, K, 256, 8>(a, B, s);
       else launch_pair_t<S, K, 256, 2>(a, B, s);
-      return;
-    }
-  }
-  if constexpr (S::NP == 1) {
-    // bf16, TTS_MI355X_PAIR32_GEO=9 (A/B): 32 channels as 2 waves of 32 x 128 on 256 columns
-    static const bool g9 = [] {
-      const char* e = std::getenv("TTS_MI355X_PAIR32_GEO");
-      return e && e[0] == '9';
-    }();
-    if (C == 32 && g9) {
-      launch_pair_t<S, K, 32, 9>(a, B, s);
       return;
     }
   }
